@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident ICRC throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 1 Mi x 4 KiB-MTU RDMA WRITE_MIDDLE packets (L = 4156 B:
+IPv4 20 + UDP 8 + BTH 12 + RETH 16 + 4096 payload + ICRC 4), synthesised on the device with
+the reference's PacketWriter field layout; one "step" = one ICRC-compute pass (kernel launch)
+over the whole batch, inputs resident in HBM, ICRCs written to an HBM array.
+
+Multi-GPU (--gpus N via torch.distributed.run): one process per GPU, each with its own
+independent QP stream of 1 Mi packets (configs[4], weak scaling, no collective on the
+data path; the only collectives are the timing barrier and a max over ranks).
+
+Prints ONE JSON line (rank 0).  value = whole-job GiB/s of packet bytes (sum of L, which
+equals the algorithmic bytes: L-4 read + 4 written per packet).  roofline = the ICRC kernel's
+achieved GB/s (HIP events on the launch stream) vs the 8.0 TB/s HBM3E peak.  cpu_baseline =
+the CPU port of compute_icrc with a crc32fast-equivalent PCLMULQDQ core (oracle/icrc_fast.c),
+rank 0 / N=1 only, on a bounded sample of the same packets.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "open-rdma-driver_amd"), os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+
+def log(msg: str) -> None:
+    print(msg, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--pmtu", type=int, default=4096)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--extra", action="store_true",
+                    help="also time verify, mixed-MTU, 16 MiB round trip and the host-resident path")
+    return ap.parse_args()
+
+
+def dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def time_kernel(fn, steps: int, warmup: int, world: int):
+    """Warmup, barrier+sync, K timed launches (HIP events on the current stream), sync+barrier.
+    Returns (wall seconds, max over ranks; kernel ms per launch from events)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    return wall, ev0.elapsed_time(ev1) / steps
+
+
+def main() -> int:
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import icrc_amd
+    from icrc_amd import workloads
+
+    eng = icrc_amd.Engine(local)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # ---- C1 workload: one QP stream per rank (dqpn = 2 + rank, distinct payload seed) ----
+    n = args.packets
+    w = workloads.write_middle_stream(n, args.pmtu, dqpn=2 + rank, payload_key=0x5EED5EED + rank)
+    L = int(w.lens[0])
+    d_buf = torch.empty(w.total_bytes, dtype=torch.uint8, device="cuda")
+    d_hdr, d_desc = dev(w.hdr), dev(w.desc.view(np.uint8))
+    eng.synth(d_buf.data_ptr(), d_desc.data_ptr(), d_hdr.data_ptr(), n, stream=stream)
+    del d_hdr, d_desc
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), False, stream)
+
+    wall, kms = time_kernel(step, args.steps, args.warmup, world)
+    bytes_per_step = n * L
+    value = world * bytes_per_step * args.steps / wall / GIB
+    achieved = bytes_per_step / (kms * 1e-3) / 1e9
+
+    result = {
+        "metric": "device-resident ICRC GiB/s over 4 KiB-MTU packet batches; % of HBM-read roofline",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-synthesised RDMA WRITE_MIDDLE packets, splitmix64 payload)",
+        "config": {
+            "workload": "configs[1]: 1Mi x 4KiB-MTU packets per GPU, device-resident ICRC compute"
+                        + (f" (configs[4]: {world} independent QP streams, one per GPU)" if world > 1 else ""),
+            "packets_per_gpu": n,
+            "packet_bytes": L,
+            "pmtu": args.pmtu,
+            "bytes_per_gpu_per_step": bytes_per_step,
+            "parallelism": f"shard-per-gpu x{world} (no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "icrc_batch_kernel<kCompute>",
+            "kernel_ms": round(kms, 4),
+        },
+    }
+
+    # ---- CPU baseline: rank 0, N = 1 only ----
+    parity = True
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle as orc  # the checker / CPU port: used only in this leg
+
+        cs = min(n, 16384)  # 68 MB sample of the same packets
+        host = d_buf[: cs * L].cpu().numpy()
+        secs, passes = 0.0, 0
+        cpu_out = None
+        while secs < args.cpu_seconds or passes == 0:
+            s, cpu_out = orc.fast_icrc_strided_timed(host, L, L, cs, threads=1)
+            secs += s
+            passes += 1
+        cpu_ok = bool(np.array_equal(cpu_out, d_out[:cs].cpu().numpy().view(np.uint32)))
+        parity = cpu_ok
+        result["cpu_baseline"] = {
+            "value": round(cs * L * passes / secs / GIB, 3),
+            "unit": "GiB/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"{cs} x {L}-B packets of the same batch, {passes} passes, {secs:.1f} s; "
+                      "compute_icrc with a crc32fast-1.4.2-equivalent PCLMULQDQ core "
+                      f"(oracle/icrc_fast.c); matches GPU: {cpu_ok}",
+        }
+        result["parity_sample_ok"] = cpu_ok
+
+    if args.extra:
+        result["extra"] = extra_measurements(eng, stream, args, world)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if parity else 1
+
+
+def extra_measurements(eng, stream, args, world):
+    """Secondary configs: verify pass, mixed MTU (configs[2]), 16 MiB round trip
+    (configs[3]) and the host-resident (PCIe) rate."""
+    import icrc_amd
+    from icrc_amd import workloads
+
+    ex = {}
+    # verify over the C1 batch with trailers written
+    n = args.packets
+    w = workloads.write_middle_stream(n, args.pmtu)
+    L = int(w.lens[0])
+    d_buf = torch.empty(w.total_bytes, dtype=torch.uint8, device="cuda")
+    eng.synth(d_buf.data_ptr(), dev(w.desc.view(np.uint8)).data_ptr(), dev(w.hdr).data_ptr(), n, stream=stream)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), True, stream)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    wall, kms = time_kernel(lambda: eng.verify_strided(d_buf.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream),
+                            args.steps, args.warmup, world)
+    ex["verify_c1"] = {"GiB/s": round(n * L / (kms * 1e-3) / GIB, 1), "kernel_ms": round(kms, 4),
+                       "all_ok": bool((d_ok == 1).all().item())}
+    del d_buf, d_out, d_ok
+
+    # mixed MTU
+    wm = workloads.mixed_mtu_stream(4 << 20)
+    d_buf = torch.empty(wm.total_bytes, dtype=torch.uint8, device="cuda")
+    eng.synth(d_buf.data_ptr(), dev(wm.desc.view(np.uint8)).data_ptr(), dev(wm.hdr).data_ptr(), wm.n, stream=stream)
+    d_off, d_len = dev(wm.off), dev(wm.lens)
+    d_out = torch.zeros(wm.n, dtype=torch.int32, device="cuda")
+    wall, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n,
+                                                      d_out.data_ptr(), False, 0, stream),
+                            args.steps, args.warmup, world)
+    tot = int(wm.lens.astype(np.uint64).sum())
+    ex["mixed_mtu_c2"] = {"packets": wm.n, "bytes": tot, "GiB/s": round(tot / (kms * 1e-3) / GIB, 1),
+                          "kernel_ms": round(kms, 4)}
+    del d_buf, d_out, d_off, d_len
+
+    # 16 MiB WRITE round trip: compute(send, write trailer) + verify(recv)
+    w3 = workloads.write_message(16 << 20, 4096)
+    d_buf = torch.empty(w3.total_bytes, dtype=torch.uint8, device="cuda")
+    eng.synth(d_buf.data_ptr(), dev(w3.desc.view(np.uint8)).data_ptr(), dev(w3.hdr).data_ptr(), w3.n, stream=stream)
+    d_off, d_len = dev(w3.off), dev(w3.lens)
+    d_out = torch.zeros(w3.n, dtype=torch.int32, device="cuda")
+    d_ok = torch.zeros(w3.n, dtype=torch.uint8, device="cuda")
+
+    def rt():
+        eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_out.data_ptr(), True, 0, stream)
+        eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), False, 0, stream)
+
+    wall, kms = time_kernel(rt, args.steps, args.warmup, world)
+    tot3 = int(w3.lens.astype(np.uint64).sum())
+    ex["roundtrip_16MiB_c3"] = {"packets": w3.n, "ms_per_roundtrip": round(kms, 4),
+                                "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1),
+                                "all_ok": bool((d_ok == 1).all().item())}
+    del d_buf
+
+    # host-resident: packets in pinned host memory -> H2D -> kernel -> D2H of ICRCs
+    nh = min(args.packets, 1 << 18)
+    wh = workloads.write_middle_stream(nh, args.pmtu)
+    Lh = int(wh.lens[0])
+    d_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, device="cuda")
+    eng.synth(d_buf.data_ptr(), dev(wh.desc.view(np.uint8)).data_ptr(), dev(wh.hdr).data_ptr(), nh, stream=stream)
+    h_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, pin_memory=True)
+    h_buf.copy_(d_buf)
+    h_out = torch.empty(nh, dtype=torch.int32, pin_memory=True)
+    d_out = torch.zeros(nh, dtype=torch.int32, device="cuda")
+
+    def h2d():
+        d_buf.copy_(h_buf, non_blocking=True)
+        eng.compute_strided(d_buf.data_ptr(), Lh, Lh, nh, d_out.data_ptr(), False, stream)
+        h_out.copy_(d_out, non_blocking=True)
+
+    wall, kms = time_kernel(h2d, max(3, args.steps // 4), 1, world)
+    ex["host_resident_pcie"] = {"packets": nh, "GiB/s": round(nh * Lh / (kms * 1e-3) / GIB, 2),
+                                "note": "pinned H2D + kernel + D2H of ICRCs, serialised on one stream"}
+    return ex
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,183 @@
+/*
+ * include/icrc.h — C-ABI of the MI355X ICRC engine (libicrc_amd.so).
+ *
+ * The drop-in boundary for the RoCEv2 Invariant-CRC path of Foreverhighness/open-rdma-driver.
+ * Every entry point cites the reference interface it replaces (paths relative to the
+ * reference root):
+ *
+ *   compute_icrc(&[u8]) -> u32
+ *       blue-rdma-device/src/third_party/net/packet_processor.rs:275-301
+ *       (identical copy: rust_driver/src/device/software/packet_processor.rs:275-301,
+ *        and rust_driver/src/responser.rs:284-307 `calculate_icrc`)
+ *   is_icrc_valid(&mut [u8]) -> Result<bool, PacketProcessorError>
+ *       packet_processor.rs:341-353
+ *   PacketWriter::{new,src_addr,src_port,dest_addr,dest_port,ip_id,message,write}
+ *       packet_processor.rs:150-265 (+ write_ip_udp_header 303-332)
+ *
+ * Plain pointers and sizes only; no HIP or torch types appear in the signatures (a HIP
+ * stream is passed as an opaque `void*`, i.e. a hipStream_t; NULL = the engine's stream).
+ *
+ * Conventions
+ *   - A packet is a full IPv4 datagram (no Ethernet header) starting at the IPv4 header;
+ *     `len` is the IPv4 total length INCLUDING the 4-byte ICRC trailer, whose contents
+ *     are ignored by compute.  The ICRC is stored little-endian at [len-4, len).
+ *   - Return codes: 0 = OK, negative = error (ICRC_E*).  A CRC mismatch is a result
+ *     (ok = 0), never an error.  Nothing aborts; the reference's panics (len < 44) map to
+ *     ICRC_EINVAL.
+ *   - The caller owns every buffer.  Synchronous calls retain no pointer; *_device calls
+ *     borrow their pointers until the stream they were issued on is synchronised.
+ *   - All entry points are reentrant (per-thread streams/staging, lock-protected registry).
+ *   - Every CRC is computed by the HIP kernel on the GPU; there is no CPU fallback.  With
+ *     no usable GPU the calls return ICRC_ENODEV.
+ */
+#ifndef ICRC_AMD_ICRC_H
+#define ICRC_AMD_ICRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICRC_OK 0
+#define ICRC_EINVAL (-22)  /* bad argument: NULL, len < 44 (reference panics), n too big */
+#define ICRC_ENOMEM (-12)  /* host or device allocation failed                           */
+#define ICRC_ENODEV (-19)  /* no usable GPU / engine for the requested device             */
+#define ICRC_EDEVICE (-5)  /* a HIP runtime call failed                                   */
+/* PacketWriter errors (PacketProcessorError, packet_processor.rs:127-148) */
+#define ICRC_EBUFFER_NOT_LARGE (-1000) /* BufferNotLargeEnough(usize)                     */
+#define ICRC_ELENGTH_TOO_LONG (-1001)  /* LengthTooLong(usize)                            */
+#define ICRC_EINVALID_METADATA (-1002) /* PacketError::InvalidMetadataType                */
+#define ICRC_EINVALID_OPCODE (-1003)   /* PacketError::InvalidOpcode                      */
+
+/* Minimum packet: IPv4(20) + UDP(8) + BTH(12) + ICRC(4) (CommonPacketHeader + ICRC_SIZE). */
+#define ICRC_MIN_PACKET 44u
+/* verify result byte values */
+#define ICRC_VERIFY_MISMATCH 0u
+#define ICRC_VERIFY_OK 1u
+#define ICRC_VERIFY_BADLEN 0xFFu /* device batches: len < 44 (counted in *d_nerr) */
+
+typedef struct icrc_engine icrc_engine;
+
+/* ---- engine lifetime ------------------------------------------------------------------ */
+/* One engine per GPU: owns the 160 KiB LDS table image in HBM, a stream and staging. */
+int icrc_engine_create(int device, icrc_engine **out);
+int icrc_engine_destroy(icrc_engine *engine);
+/* Lazily created, lock-protected default engine for `device` (-1 = current HIP device). */
+int icrc_engine_default(int device, icrc_engine **out);
+int icrc_engine_device_ordinal(const icrc_engine *engine);
+/* Number of HIP devices visible (0 when no GPU); never fails. */
+int icrc_device_count(void);
+/* Static library/kernel description (for logs): "icrc_amd <ver> gfx950 ..." */
+const char *icrc_version(void);
+
+/* ---- scalar drop-ins (replace compute_icrc / is_icrc_valid) ---------------------------- */
+/* compute_icrc, packet_processor.rs:275-301.  Returns the ICRC; *err (may be NULL) gets
+ * ICRC_OK or an error code (then the return value is 0). */
+uint32_t icrc_compute(const uint8_t *pkt, size_t len, int *err);
+/* is_icrc_valid, packet_processor.rs:341-353.  *ok = 1 when the trailer matches.
+ * zero_trailer != 0 reproduces the reference's in-place zeroing of the trailer (350). */
+int icrc_verify(uint8_t *pkt, size_t len, int zero_trailer, int *ok);
+
+/* ---- host-resident batches (packets in host memory: descriptor rings, wire buffers) ---- */
+/* Packet i is base[off[i] .. off[i]+len[i]).  write_trailer != 0 stores each ICRC LE into
+ * its packet's last 4 bytes (what PacketWriter::write does, packet_processor.rs:260-263). */
+int icrc_compute_batch(uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n,
+                       uint32_t *out_icrc, int write_trailer);
+/* ok[i] = 1/0 per packet (one byte each).  zero_trailer as icrc_verify. */
+int icrc_verify_batch(uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n,
+                      uint8_t *ok, int zero_trailer);
+int icrc_compute_batch_ex(icrc_engine *engine, uint8_t *base, const uint64_t *off,
+                          const uint32_t *len, uint32_t n, uint32_t *out_icrc, int write_trailer);
+int icrc_verify_batch_ex(icrc_engine *engine, uint8_t *base, const uint64_t *off,
+                         const uint32_t *len, uint32_t n, uint8_t *ok, int zero_trailer);
+
+/* ---- device-resident batches (all pointers are device pointers; async on `stream`) ----- */
+/* d_off/d_len: per-packet (offset, len).  d_out (may be NULL) receives the ICRCs.
+ * d_nerr (may be NULL): device uint32 counter incremented once per packet with len < 44
+ * (its ICRC is reported as 0 and nothing is written to that packet). */
+int icrc_compute_batch_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d_off,
+                              const uint32_t *d_len, uint32_t n, uint32_t *d_out,
+                              int write_trailer, uint32_t *d_nerr, void *stream);
+int icrc_verify_batch_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d_off,
+                             const uint32_t *d_len, uint32_t n, uint8_t *d_ok, int zero_trailer,
+                             uint32_t *d_nerr, void *stream);
+/* Uniform batches: packet i at d_base + i*stride, every packet `len` bytes. */
+int icrc_compute_strided_device(icrc_engine *engine, uint8_t *d_base, uint64_t stride,
+                                uint32_t len, uint32_t n, uint32_t *d_out, int write_trailer,
+                                void *stream);
+int icrc_verify_strided_device(icrc_engine *engine, uint8_t *d_base, uint64_t stride,
+                               uint32_t len, uint32_t n, uint8_t *d_ok, int zero_trailer,
+                               void *stream);
+
+/* ---- packet synthesis on the device (bench inputs; precursor of the fused packetizer) --- */
+/* Packet i = header template d_hdr[hdr_index*64 .. +hdr_len) ‖ payload ‖ zero pad ‖ zero
+ * ICRC slot, written at d_base + offset.  Payload byte q = byte ((pos+q) & 7) of
+ * splitmix64_mix(payload_key + ((pos+q) >> 3)) — the same function as the oracle's
+ * oracle_mix64 — so that host and device synthesise identical bytes. */
+typedef struct icrc_synth_desc {
+    uint64_t offset;
+    uint64_t payload_key;
+    uint64_t payload_pos;
+    uint32_t hdr_len;     /* <= 64, multiple of 4 */
+    uint32_t payload_len; /* bytes before pad */
+    uint32_t total_len;   /* L (IPv4 total length incl. ICRC) */
+    uint32_t hdr_index;
+} icrc_synth_desc;
+int icrc_synth_device(icrc_engine *engine, uint8_t *d_base, const icrc_synth_desc *d_desc,
+                      const uint8_t *d_hdr, uint32_t n, void *stream);
+
+/* ---- packet writer (PacketWriter, packet_processor.rs:150-265) -------------------------- */
+/* Flattened RdmaMessage (third_party/net/types.rs; Metadata::General / ::Acknowledge). */
+typedef struct icrc_rdma_msg {
+    uint8_t kind;   /* 0 = Metadata::General, 1 = Metadata::Acknowledge */
+    uint8_t opcode; /* ToHostWorkRbDescOpcode (third_party/queues.rs:393-425) */
+    uint8_t tran_type; /* ToHostWorkRbDescTransType, RC = 0 */
+    uint8_t solicited;
+    uint8_t ack_req;
+    uint8_t aeth_code;
+    uint8_t aeth_value;
+    uint8_t has_imm;
+    uint8_t has_secondary_reth;
+    uint8_t _pad0[3];
+    uint16_t pkey;
+    uint16_t _pad1;
+    uint32_t dqpn;
+    uint32_t psn;
+    uint32_t msn;
+    uint32_t imm;
+    uint64_t reth_va;
+    uint32_t reth_rkey;
+    uint32_t reth_len;
+    uint64_t sec_va;
+    uint32_t sec_rkey;
+    uint32_t sec_len;
+    const uint8_t *payload; /* one scatter-gather element (PayloadInfo) */
+    uint64_t payload_len;
+} icrc_rdma_msg;
+
+/* Header bytes only (IPv4/UDP/BTH/ext) into buf[0 .. 28+hdr); no payload, no ICRC.
+ * *out_hdr_len = 28 + header length; *out_total_len = L.  Used to build synth templates. */
+int icrc_packet_headers(uint8_t *buf, size_t buf_len, const icrc_rdma_msg *msg, uint32_t src_ip,
+                        uint16_t src_port, uint32_t dst_ip, uint16_t dst_port, uint16_t ip_id,
+                        size_t *out_hdr_len, size_t *out_total_len);
+/* PacketWriter::write: headers + payload + ICRC (ICRC on the GPU).  *out_len = L. */
+int icrc_packet_write(uint8_t *buf, size_t buf_len, const icrc_rdma_msg *msg, uint32_t src_ip,
+                      uint16_t src_port, uint32_t dst_ip, uint16_t dst_port, uint16_t ip_id,
+                      size_t *out_len);
+/* write_ip_udp_header, packet_processor.rs:307-332 (addresses in host order a<<24|..|d). */
+void icrc_write_ip_udp_header(uint8_t *buf, uint32_t src_ip, uint16_t src_port, uint32_t dst_ip,
+                              uint16_t dst_port, uint16_t total_length, uint16_t ip_id);
+/* Header composite length (BTH + extension headers) for an opcode (packet.rs:427-438), or
+ * ICRC_EINVALID_OPCODE. */
+int icrc_rdma_header_len(uint8_t opcode);
+
+/* ---- host-only helpers (no GPU needed) -------------------------------------------------- */
+/* The 160 KiB LDS table image the kernel uploads (layout documented in DESIGN.md). */
+int icrc_table_image(uint32_t *out_words, uint32_t nwords);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICRC_AMD_ICRC_H */

@@ -1,0 +1,50 @@
+// icrc_internal.h — shared between the HIP kernels (icrc_kernels.hip) and the host engine.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "icrc.h"
+
+namespace icrc {
+
+// ---- LDS table image (identical layout in HBM and in LDS; copied linearly per workgroup) --
+// Bulk tables B_b (b = 0..3): B_b[x] = M^64(x << 8b), M = "advance the reflected CRC-32
+// state over 4 zero bytes".  32 copies, one per ds_read_b32 bank, so lane l always reads
+// bank (l & 31):  byte address = (b >> 1) * 65536 + x * 256 + (b & 1) * 128 + (l & 31) * 4.
+// Final per-lane tables F_l (l = 0..63): F_l[n][v] = M^(64-l)(v << 4n), nibble-indexed:
+//   byte address = kFinalBase + (n * 16 + v) * 256 + l * 4.
+constexpr uint32_t kLdsBytes = 163840;  // 160 KiB: the whole CU LDS
+constexpr uint32_t kFinalBase = 131072;
+constexpr uint32_t kLdsWords = kLdsBytes / 4;
+
+// Host: fill a kLdsWords image.
+void build_table_image(uint32_t *img);
+// Host reference helpers used by the table builder (exposed for unit tests).
+uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
+
+// ---- kernel launch parameters ------------------------------------------------------------
+struct BatchParams {
+    uint8_t *base;
+    const uint64_t *off;  // nullptr => strided (offset = i * stride)
+    const uint32_t *len;  // nullptr => uniform length ulen
+    uint64_t stride;
+    uint32_t ulen;
+    uint32_t n;
+    uint32_t *out;   // compute: ICRC per packet (may be null)
+    uint8_t *ok;     // verify: 1/0/0xFF per packet
+    uint32_t *nerr;  // may be null
+    const uint32_t *table;  // kLdsWords image in device memory
+    int trailer;     // compute: write trailer; verify: zero trailer
+};
+
+enum Mode : int { kCompute = 0, kVerify = 1 };
+
+constexpr int kWavesPerGroup = 16;                // 1024-thread workgroup, 1 per CU (LDS-bound)
+constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
+
+// Launch wrappers (icrc_kernels.hip).  `grid` = number of workgroups.
+int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
+int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
+                 void *stream);
+
+}  // namespace icrc

@@ -1,0 +1,298 @@
+// icrc_kernels.hip — CDNA4 (gfx950) kernels of the ICRC engine.
+//
+// What is computed (bit-exact with the reference compute_icrc,
+// blue-rdma-device/src/third_party/net/packet_processor.rs:275-301):
+//
+//   icrc(pkt, L) = CRC32_ISO_HDLC( FF x 8 ‖ mask(pkt[0..40)) ‖ pkt[40 .. L-4) )
+//   mask: bytes 1, 8, 10, 11, 26, 27, 32 := 0xFF   (packet.rs:140-142, 443-498)
+//
+// Restated as a raw (init 0, no xorout) reflected CRC over the word stream
+//   u_0 = FF FF FF FF,  u_k = masked pkt word k-1  (k = 1 .. N-1, N = 1 + (L-4)/4)
+// because init 0xFFFFFFFF over a message that starts with FF x 4 cancels to zeros, and
+// leading zero words do not move a raw CRC.  With M = "advance the state over 4 zero
+// bytes" (a GF(2)-linear map):   S = XOR_k M^(N-k)(u_k),   icrc = ~S.
+//
+// Mapping (one wavefront per packet): the stream is END-aligned into rows of 64 words;
+// lane l of row r holds word k = k0 + 64 r + l (k0 = N - 64 R <= 0, words k < 0 are the
+// free leading zeros).  Each row is one coalesced 256-byte buffer_load_dword per lane.
+// Lane l keeps a Horner accumulator over its word column,
+//     acc_l <- M^64(acc_l) ^ u          (4 LDS table lookups: M^64 is byte-sliced)
+// and at the end the packet state is   S = XOR_l M^(64-l)(acc_l)   — the per-lane
+// multiplier depends only on the lane (the stream is end-aligned), applied with 8
+// nibble lookups into per-lane tables, then an XOR reduction across the wavefront.
+// No MFMA: this is GF(2) arithmetic; the bound is HBM bandwidth.
+//
+// LDS holds 160 KiB of tables (layout in icrc_internal.h): the bulk tables are replicated
+// 32x so that lane l always reads bank (l & 31) — conflict-free ds_read_b32.
+#include <hip/hip_runtime.h>
+
+#include "icrc_internal.h"
+
+namespace icrc {
+namespace {
+
+constexpr int kGroup = 16;  // rows (each 256 B per wave) whose loads are issued together
+
+__device__ __forceinline__ uint32_t lds_at(const char *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
+}
+
+struct LaneConsts {
+    uint32_t lo0, lo1, lo2, lo3;  // bulk-table lane slots for bytes 0..3
+    uint32_t fin;                 // per-lane final-table base
+};
+
+// M^64(s): four byte lookups (bytes are placed directly at address bits 8..15).
+__device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const LaneConsts &c) {
+    const uint32_t a0 = ((s << 8) & 0xff00u) | c.lo0;
+    const uint32_t a1 = (s & 0xff00u) | c.lo1;
+    const uint32_t a2 = ((s >> 8) & 0xff00u) | c.lo2;
+    const uint32_t a3 = ((s >> 16) & 0xff00u) | c.lo3;
+    return lds_at(lds, a0) ^ lds_at(lds, a1) ^ lds_at(lds, a2) ^ lds_at(lds, a3);
+}
+
+// M^(64-lane)(acc) via 8 nibble lookups into this lane's private tables.
+__device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uint32_t fin) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r ^= lds_at(lds, fin + n * 4096u + (((acc >> (4 * n)) & 15u) << 8));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x ^= __shfl_xor(x, m, 64);
+    return x;
+}
+
+// Fast path (4-aligned packet, L % 4 == 0): OR-masks of the stream words that carry the
+// FF prefix (k = 0) and the masked header bytes (packet.rs offsets 1, 8, 10-11, 26-27, 32).
+__device__ __forceinline__ uint32_t head_mask(int k) {
+    return k == 0   ? 0xffffffffu
+           : k == 1 ? 0x0000ff00u
+           : k == 3 ? 0xffff00ffu
+           : k == 7 ? 0xffff0000u
+           : k == 9 ? 0x000000ffu
+                    : 0u;
+}
+
+__device__ __forceinline__ uint32_t fast_packet_state(const char *lds, const uint8_t *pkt,
+                                                      uint32_t Ld, const LaneConsts &c,
+                                                      uint32_t lane) {
+    const int N = 1 + static_cast<int>(Ld >> 2);
+    const int R = (N + 63) >> 6;
+    const int k0 = N - 64 * R;
+    // Out-of-range words (k < 1, i.e. before the packet) read as 0 through the descriptor.
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(pkt), 0, static_cast<int>(Ld), 0x00020000);
+    const uint32_t vbase = 4u * static_cast<uint32_t>(k0 - 1 + static_cast<int>(lane));
+    uint32_t acc = 0;
+    for (int g = 0; g < R; g += kGroup) {
+        uint32_t u[kGroup];
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j)
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * static_cast<uint32_t>(g + j)), 0, 0);
+        if (g == 0) {
+            const int k = k0 + static_cast<int>(lane);
+            u[0] |= head_mask(k);
+            u[1] |= head_mask(k + 64);
+            acc = u[0];
+#pragma unroll
+            for (int j = 1; j < kGroup; ++j)
+                if (j < R) acc = mul_m64(lds, acc, c) ^ u[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < kGroup; ++j)
+                if (g + j < R) acc = mul_m64(lds, acc, c) ^ u[j];
+        }
+    }
+    return acc;
+}
+
+// Generic path: any alignment, any length >= 44.  The stream is front-padded with
+// z = (-(4 + Ld)) mod 4 zero bytes (free leading zeros) so that it ends on a word.
+__device__ __forceinline__ uint32_t slow_word(const uint8_t *pkt, int k, int z) {
+    if (k < 0) return 0u;
+    uint32_t w = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = 4 * k + t - z;  // index in FF x 4 ‖ masked packet
+        uint32_t b;
+        if (j < 0) {
+            b = 0u;
+        } else if (j < 4) {
+            b = 0xffu;
+        } else {
+            const uint32_t o = static_cast<uint32_t>(j - 4);
+            b = pkt[o];
+            if (o == 1 || o == 8 || o == 10 || o == 11 || o == 26 || o == 27 || o == 32) b = 0xffu;
+        }
+        w |= b << (8 * t);
+    }
+    return w;
+}
+
+__device__ __forceinline__ uint32_t slow_packet_state(const char *lds, const uint8_t *pkt,
+                                                      uint32_t Ld, const LaneConsts &c,
+                                                      uint32_t lane) {
+    const uint32_t T = 4u + Ld;
+    const int z = static_cast<int>((4u - (T & 3u)) & 3u);
+    const int N = static_cast<int>((T + static_cast<uint32_t>(z)) >> 2);
+    const int R = (N + 63) >> 6;
+    const int k0 = N - 64 * R;
+    uint32_t acc = 0;
+    for (int r = 0; r < R; ++r) {
+        const uint32_t u = slow_word(pkt, k0 + 64 * r + static_cast<int>(lane), z);
+        acc = (r == 0) ? u : (mul_m64(lds, acc, c) ^ u);
+    }
+    return acc;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.lo0 = (lane & 31u) * 4u;
+    c.lo1 = c.lo0 + 128u;
+    c.lo2 = c.lo0 + 65536u;
+    c.lo3 = c.lo1 + 65536u;
+    c.fin = kFinalBase + lane * 4u;
+
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    for (uint32_t i = blockIdx.x * kWavesPerGroup + wave; i < p.n; i += tw) {
+        const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
+        const uint32_t L = p.len ? p.len[i] : p.ulen;
+        uint8_t *pkt = p.base + off;
+        if (L < ICRC_MIN_PACKET) {
+            if (lane == 0) {
+                if (p.nerr) atomicAdd(p.nerr, 1u);
+                if (MODE == kCompute) {
+                    if (p.out) p.out[i] = 0u;
+                } else {
+                    p.ok[i] = ICRC_VERIFY_BADLEN;
+                }
+            }
+            continue;
+        }
+        const uint32_t Ld = L - 4u;
+        const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
+        const uint32_t acc = fast ? fast_packet_state(lds, pkt, Ld, c, lane)
+                                  : slow_packet_state(lds, pkt, Ld, c, lane);
+        const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
+        if (lane == 0) {
+            uint8_t *tr = pkt + Ld;
+            if (MODE == kCompute) {
+                if (p.out) p.out[i] = crc;
+                if (p.trailer) {
+                    if (fast) {
+                        *reinterpret_cast<uint32_t *>(tr) = crc;
+                    } else {
+                        tr[0] = static_cast<uint8_t>(crc);
+                        tr[1] = static_cast<uint8_t>(crc >> 8);
+                        tr[2] = static_cast<uint8_t>(crc >> 16);
+                        tr[3] = static_cast<uint8_t>(crc >> 24);
+                    }
+                }
+            } else {
+                uint32_t stored;
+                if (fast) {
+                    stored = *reinterpret_cast<const uint32_t *>(tr);
+                } else {
+                    stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                             (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+                }
+                p.ok[i] = (stored == crc) ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+                if (p.trailer) {
+                    if (fast) {
+                        *reinterpret_cast<uint32_t *>(tr) = 0u;
+                    } else {
+                        tr[0] = tr[1] = tr[2] = tr[3] = 0;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---- packet synthesis ----------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint32_t synth_byte(const icrc_synth_desc &d, const uint8_t *hdr, uint32_t q) {
+    if (q < d.hdr_len) return hdr[static_cast<uint64_t>(d.hdr_index) * 64u + q];
+    const uint32_t pq = q - d.hdr_len;
+    if (pq < d.payload_len) {
+        const uint64_t pos = d.payload_pos + pq;
+        return static_cast<uint32_t>(mix64(d.payload_key + (pos >> 3)) >> (8u * static_cast<uint32_t>(pos & 7u))) & 0xffu;
+    }
+    return 0u;
+}
+
+__global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const icrc_synth_desc *desc,
+                                                          const uint8_t *hdr, uint32_t n) {
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const icrc_synth_desc d = desc[i];
+        uint8_t *pkt = base + d.offset;
+        const uint32_t nw = d.total_len >> 2;
+        const bool aligned = ((reinterpret_cast<uintptr_t>(pkt) | d.payload_pos) & 3u) == 0;
+        for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+            const uint32_t b0 = 4u * w;
+            uint32_t val;
+            if (aligned && b0 + 4u <= d.hdr_len) {
+                val = *reinterpret_cast<const uint32_t *>(hdr + static_cast<uint64_t>(d.hdr_index) * 64u + b0);
+            } else if (aligned && b0 >= d.hdr_len && b0 + 4u <= d.hdr_len + d.payload_len) {
+                const uint64_t pos = d.payload_pos + (b0 - d.hdr_len);
+                val = static_cast<uint32_t>(mix64(d.payload_key + (pos >> 3)) >> (8u * static_cast<uint32_t>(pos & 7u)));
+            } else {
+                val = synth_byte(d, hdr, b0) | (synth_byte(d, hdr, b0 + 1) << 8) |
+                      (synth_byte(d, hdr, b0 + 2) << 16) | (synth_byte(d, hdr, b0 + 3) << 24);
+            }
+            if (aligned) {
+                *reinterpret_cast<uint32_t *>(pkt + b0) = val;
+            } else {
+                pkt[b0] = static_cast<uint8_t>(val);
+                pkt[b0 + 1] = static_cast<uint8_t>(val >> 8);
+                pkt[b0 + 2] = static_cast<uint8_t>(val >> 16);
+                pkt[b0 + 3] = static_cast<uint8_t>(val >> 24);
+            }
+        }
+        for (uint32_t q = (nw << 2) + threadIdx.x; q < d.total_len; q += blockDim.x)
+            pkt[q] = static_cast<uint8_t>(synth_byte(d, hdr, q));
+    }
+}
+
+}  // namespace
+
+int launch_batch(int mode, const BatchParams &p, int grid, void *stream) {
+    if (grid < 1) grid = 1;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode == kCompute)
+        hipLaunchKernelGGL(icrc_batch_kernel<kCompute>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    else
+        hipLaunchKernelGGL(icrc_batch_kernel<kVerify>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
+                 void *stream) {
+    if (n == 0) return ICRC_OK;
+    const uint32_t grid = n < 65536u ? n : 65536u;
+    hipLaunchKernelGGL(icrc_synth_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       base, desc, hdr, n);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+}  // namespace icrc

@@ -1,0 +1,343 @@
+"""icrc_amd — Python binding of the MI355X ICRC engine (libicrc_amd.so, C-ABI include/icrc.h).
+
+Host-side mirror of the reference's packet/ICRC surface
+(blue-rdma-device/src/third_party/net/packet_processor.rs):
+
+    compute_icrc(data) -> int              packet_processor.rs:275-301
+    is_icrc_valid(buf) -> bool             packet_processor.rs:341-353 (zeroes the trailer)
+    PacketWriter(buf).src_addr(..)...write()   packet_processor.rs:150-265
+    write_ip_udp_header(...)               packet_processor.rs:303-332
+
+plus batch / device-resident entry points.  Every CRC runs in the HIP kernel; if the
+shared library is missing this module raises at import time (no silent fallback), and
+with no GPU every compute call raises IcrcError(ENODEV).
+"""
+from __future__ import annotations
+
+import ctypes
+import ipaddress
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd.so")
+
+OK = 0
+EINVAL = -22
+ENOMEM = -12
+ENODEV = -19
+EDEVICE = -5
+EBUFFER_NOT_LARGE = -1000
+ELENGTH_TOO_LONG = -1001
+EINVALID_METADATA = -1002
+EINVALID_OPCODE = -1003
+MIN_PACKET = 44
+ICRC_SIZE = 4
+RDMA_PORT = 4791  # blue-rdma-device/src/net.rs:11
+LDS_WORDS = 163840 // 4
+
+VERIFY_MISMATCH = 0
+VERIFY_OK = 1
+VERIFY_BADLEN = 0xFF
+
+_ERRNAMES = {
+    EINVAL: "EINVAL", ENOMEM: "ENOMEM", ENODEV: "ENODEV", EDEVICE: "EDEVICE",
+    EBUFFER_NOT_LARGE: "BufferNotLargeEnough", ELENGTH_TOO_LONG: "LengthTooLong",
+    EINVALID_METADATA: "InvalidMetadataType", EINVALID_OPCODE: "InvalidOpcode",
+}
+
+
+class IcrcError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        super().__init__(f"{what}: {_ERRNAMES.get(rc, rc)} ({rc})")
+
+
+class RdmaMsg(ctypes.Structure):
+    """icrc_rdma_msg — flattened RdmaMessage (third_party/net/types.rs)."""
+
+    _fields_ = [
+        ("kind", ctypes.c_uint8), ("opcode", ctypes.c_uint8), ("tran_type", ctypes.c_uint8),
+        ("solicited", ctypes.c_uint8), ("ack_req", ctypes.c_uint8), ("aeth_code", ctypes.c_uint8),
+        ("aeth_value", ctypes.c_uint8), ("has_imm", ctypes.c_uint8),
+        ("has_secondary_reth", ctypes.c_uint8), ("_pad0", ctypes.c_uint8 * 3),
+        ("pkey", ctypes.c_uint16), ("_pad1", ctypes.c_uint16), ("dqpn", ctypes.c_uint32),
+        ("psn", ctypes.c_uint32), ("msn", ctypes.c_uint32), ("imm", ctypes.c_uint32),
+        ("reth_va", ctypes.c_uint64), ("reth_rkey", ctypes.c_uint32), ("reth_len", ctypes.c_uint32),
+        ("sec_va", ctypes.c_uint64), ("sec_rkey", ctypes.c_uint32), ("sec_len", ctypes.c_uint32),
+        ("payload", ctypes.c_void_p), ("payload_len", ctypes.c_uint64),
+    ]
+
+
+class SynthDesc(ctypes.Structure):
+    """icrc_synth_desc (include/icrc.h)."""
+
+    _fields_ = [
+        ("offset", ctypes.c_uint64), ("payload_key", ctypes.c_uint64),
+        ("payload_pos", ctypes.c_uint64), ("hdr_len", ctypes.c_uint32),
+        ("payload_len", ctypes.c_uint32), ("total_len", ctypes.c_uint32),
+        ("hdr_index", ctypes.c_uint32),
+    ]
+
+
+SYNTH_DESC_DTYPE = np.dtype([
+    ("offset", "<u8"), ("payload_key", "<u8"), ("payload_pos", "<u8"), ("hdr_len", "<u4"),
+    ("payload_len", "<u4"), ("total_len", "<u4"), ("hdr_index", "<u4"),
+])
+assert SYNTH_DESC_DTYPE.itemsize == ctypes.sizeof(SynthDesc) == 40
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"icrc_amd: native library {LIB_PATH} is missing — build it with "
+            "`make -C open-rdma-driver_amd` (or __graft_entry__.build()); there is no fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
+    sig = {
+        "icrc_engine_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "icrc_engine_destroy": (i32, [vp]),
+        "icrc_engine_default": (i32, [i32, ctypes.POINTER(vp)]),
+        "icrc_engine_device_ordinal": (i32, [vp]),
+        "icrc_device_count": (i32, []),
+        "icrc_version": (ctypes.c_char_p, []),
+        "icrc_compute": (u32, [vp, sz, ctypes.POINTER(i32)]),
+        "icrc_verify": (i32, [vp, sz, i32, ctypes.POINTER(i32)]),
+        "icrc_compute_batch": (i32, [vp, vp, vp, u32, vp, i32]),
+        "icrc_verify_batch": (i32, [vp, vp, vp, u32, vp, i32]),
+        "icrc_compute_batch_ex": (i32, [vp, vp, vp, vp, u32, vp, i32]),
+        "icrc_verify_batch_ex": (i32, [vp, vp, vp, vp, u32, vp, i32]),
+        "icrc_compute_batch_device": (i32, [vp, vp, vp, vp, u32, vp, i32, vp, vp]),
+        "icrc_verify_batch_device": (i32, [vp, vp, vp, vp, u32, vp, i32, vp, vp]),
+        "icrc_compute_strided_device": (i32, [vp, vp, u64, u32, u32, vp, i32, vp]),
+        "icrc_verify_strided_device": (i32, [vp, vp, u64, u32, u32, vp, i32, vp]),
+        "icrc_synth_device": (i32, [vp, vp, vp, vp, u32, vp]),
+        "icrc_packet_headers": (i32, [vp, sz, ctypes.POINTER(RdmaMsg), u32, ctypes.c_uint16, u32,
+                                      ctypes.c_uint16, ctypes.c_uint16, ctypes.POINTER(sz),
+                                      ctypes.POINTER(sz)]),
+        "icrc_packet_write": (i32, [vp, sz, ctypes.POINTER(RdmaMsg), u32, ctypes.c_uint16, u32,
+                                    ctypes.c_uint16, ctypes.c_uint16, ctypes.POINTER(sz)]),
+        "icrc_write_ip_udp_header": (None, [vp, u32, ctypes.c_uint16, u32, ctypes.c_uint16,
+                                            ctypes.c_uint16, ctypes.c_uint16]),
+        "icrc_rdma_header_len": (i32, [ctypes.c_uint8]),
+        "icrc_table_image": (i32, [vp, u32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise IcrcError(rc, what)
+
+
+def _u8(a) -> np.ndarray:
+    if isinstance(a, np.ndarray):
+        if a.dtype != np.uint8 or not a.flags.c_contiguous:
+            raise TypeError("expected a C-contiguous uint8 array")
+        return a
+    return np.frombuffer(bytearray(a), dtype=np.uint8)
+
+
+def ip4(addr) -> int:
+    """Ipv4Addr -> host-order u32 (a.b.c.d = a<<24|b<<16|c<<8|d)."""
+    if isinstance(addr, int):
+        return addr
+    return int(ipaddress.IPv4Address(addr))
+
+
+def device_count() -> int:
+    return lib.icrc_device_count()
+
+
+def version() -> str:
+    return lib.icrc_version().decode()
+
+
+def table_image() -> np.ndarray:
+    img = np.zeros(LDS_WORDS, dtype=np.uint32)
+    _check(lib.icrc_table_image(img.ctypes.data, img.size), "icrc_table_image")
+    return img
+
+
+# ---- the reference surface -----------------------------------------------------------------
+def compute_icrc(data) -> int:
+    """compute_icrc (packet_processor.rs:275-301).  Raises IcrcError(EINVAL) where the
+    reference would panic (len < 44)."""
+    a = _u8(data)
+    err = ctypes.c_int(0)
+    v = lib.icrc_compute(a.ctypes.data, a.size, ctypes.byref(err))
+    _check(err.value, "compute_icrc")
+    return v
+
+
+def is_icrc_valid(buf: np.ndarray, zero_trailer: bool = True) -> bool:
+    """is_icrc_valid (packet_processor.rs:341-353): zeroes the trailer in place, as the
+    reference does at 350, then recomputes and compares."""
+    a = _u8(buf)
+    ok = ctypes.c_int(0)
+    _check(lib.icrc_verify(a.ctypes.data, a.size, 1 if zero_trailer else 0, ctypes.byref(ok)),
+           "is_icrc_valid")
+    return bool(ok.value)
+
+
+def write_ip_udp_header(buf: np.ndarray, src_addr, src_port: int, dest_addr, dest_port: int,
+                        total_length: int, ip_identification: int) -> None:
+    """write_ip_udp_header (packet_processor.rs:307-332)."""
+    a = _u8(buf)
+    if a.size < 28:
+        raise ValueError("buffer smaller than IPv4+UDP headers")
+    lib.icrc_write_ip_udp_header(a.ctypes.data, ip4(src_addr), src_port, ip4(dest_addr), dest_port,
+                                 total_length & 0xFFFF, ip_identification & 0xFFFF)
+
+
+class PacketWriter:
+    """PacketWriter builder (packet_processor.rs:150-265).  write() returns the total length
+    or raises IcrcError with the PacketProcessorError code."""
+
+    def __init__(self, buf: np.ndarray):
+        self.buf = _u8(buf)
+        self._src = self._sport = self._dst = self._dport = self._ipid = self._msg = None
+
+    def src_addr(self, a):
+        self._src = ip4(a)
+        return self
+
+    def src_port(self, p: int):
+        self._sport = p
+        return self
+
+    def dest_addr(self, a):
+        self._dst = ip4(a)
+        return self
+
+    def dest_port(self, p: int):
+        self._dport = p
+        return self
+
+    def ip_id(self, i: int):
+        self._ipid = i
+        return self
+
+    def message(self, m: RdmaMsg):
+        self._msg = m
+        return self
+
+    def write(self) -> int:
+        if self._msg is None:
+            raise IcrcError(EINVAL, "PacketWriter::write: MissingMessage")
+        for name, v in (("MissingIpId", self._ipid), ("MissingSrcAddr", self._src),
+                        ("MissingSrcPort", self._sport), ("MissingDestAddr", self._dst),
+                        ("MissingDestPort", self._dport)):
+            if v is None:
+                raise IcrcError(EINVAL, f"PacketWriter::write: {name}")
+        n = ctypes.c_size_t(0)
+        _check(lib.icrc_packet_write(self.buf.ctypes.data, self.buf.size, ctypes.byref(self._msg),
+                                     self._src, self._sport, self._dst, self._dport, self._ipid,
+                                     ctypes.byref(n)), "PacketWriter::write")
+        return n.value
+
+
+def packet_headers(msg: RdmaMsg, src, sport: int, dst, dport: int, ip_id: int):
+    """Header bytes (IPv4/UDP/BTH/ext) of the packet PacketWriter would build for msg.
+    Returns (header uint8 array, total length L)."""
+    buf = np.zeros(128, dtype=np.uint8)
+    hl = ctypes.c_size_t(0)
+    tl = ctypes.c_size_t(0)
+    _check(lib.icrc_packet_headers(buf.ctypes.data, buf.size, ctypes.byref(msg), ip4(src), sport,
+                                   ip4(dst), dport, ip_id, ctypes.byref(hl), ctypes.byref(tl)),
+           "icrc_packet_headers")
+    return buf[: hl.value].copy(), tl.value
+
+
+# ---- batches ---------------------------------------------------------------------------------
+def compute_icrc_batch(base: np.ndarray, off, lens, write_trailer: bool = False) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    out = np.zeros(off.size, dtype=np.uint32)
+    _check(lib.icrc_compute_batch(_u8(base).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
+                                  out.ctypes.data, 1 if write_trailer else 0), "icrc_compute_batch")
+    return out
+
+
+def verify_icrc_batch(base: np.ndarray, off, lens, zero_trailer: bool = False) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    ok = np.zeros(off.size, dtype=np.uint8)
+    _check(lib.icrc_verify_batch(_u8(base).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
+                                 ok.ctypes.data, 1 if zero_trailer else 0), "icrc_verify_batch")
+    return ok
+
+
+class Engine:
+    """One engine per GPU (icrc_engine_create).  Device entry points take raw device pointers
+    (e.g. torch tensor .data_ptr()) and a hipStream_t handle (e.g.
+    torch.cuda.current_stream().cuda_stream); 0/None = the engine's own stream."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.icrc_engine_create(device, ctypes.byref(h)), "icrc_engine_create")
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            lib.icrc_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compute_strided(self, d_base: int, stride: int, length: int, n: int, d_out: int,
+                        write_trailer: bool = False, stream: Optional[int] = None) -> None:
+        _check(lib.icrc_compute_strided_device(self.handle, d_base, stride, length, n, d_out,
+                                               1 if write_trailer else 0, stream or None),
+               "icrc_compute_strided_device")
+
+    def verify_strided(self, d_base: int, stride: int, length: int, n: int, d_ok: int,
+                       zero_trailer: bool = False, stream: Optional[int] = None) -> None:
+        _check(lib.icrc_verify_strided_device(self.handle, d_base, stride, length, n, d_ok,
+                                              1 if zero_trailer else 0, stream or None),
+               "icrc_verify_strided_device")
+
+    def compute_batch(self, d_base: int, d_off: int, d_len: int, n: int, d_out: int,
+                      write_trailer: bool = False, d_nerr: int = 0,
+                      stream: Optional[int] = None) -> None:
+        _check(lib.icrc_compute_batch_device(self.handle, d_base, d_off, d_len, n, d_out or None,
+                                             1 if write_trailer else 0, d_nerr or None,
+                                             stream or None), "icrc_compute_batch_device")
+
+    def verify_batch(self, d_base: int, d_off: int, d_len: int, n: int, d_ok: int,
+                     zero_trailer: bool = False, d_nerr: int = 0,
+                     stream: Optional[int] = None) -> None:
+        _check(lib.icrc_verify_batch_device(self.handle, d_base, d_off, d_len, n, d_ok,
+                                            1 if zero_trailer else 0, d_nerr or None,
+                                            stream or None), "icrc_verify_batch_device")
+
+    def synth(self, d_base: int, d_desc: int, d_hdr: int, n: int,
+              stream: Optional[int] = None) -> None:
+        _check(lib.icrc_synth_device(self.handle, d_base, d_desc, d_hdr, n, stream or None),
+               "icrc_synth_device")
+
+    def compute_batch_host(self, base: np.ndarray, off, lens, write_trailer: bool = False):
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros(off.size, dtype=np.uint32)
+        _check(lib.icrc_compute_batch_ex(self.handle, _u8(base).ctypes.data, off.ctypes.data,
+                                         lens.ctypes.data, off.size, out.ctypes.data,
+                                         1 if write_trailer else 0), "icrc_compute_batch_ex")
+        return out
+
+
+from . import workloads  # noqa: E402,F401  (synthetic packet streams)

@@ -1,0 +1,146 @@
+/*
+ * oracle/icrc_oracle.h — TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
+ *
+ * CPU restatement of the reference's ICRC path (Foreverhighness/open-rdma-driver,
+ * blue-rdma-device/src/third_party/net/{packet_processor,packet,types}.rs and the emulator
+ * callers in net/util.rs + queues/send/operations/{common,write}.rs).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ *
+ * Parity pinning: the restatement is checked against the reference's own known-answer
+ * vectors (packet_processor.rs:367-388, responser.rs:348-393, net/util.rs:225-239) and
+ * against Python zlib.crc32 fixtures committed under tests/golden/.
+ *
+ * The CRC arithmetic lives in the third-party crate crc32fast 1.4.2 (Cargo.lock:230-236),
+ * which is not vendored in /root/reference; its published algorithm is CRC-32/ISO-HDLC
+ * (reflected poly 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF), restated here.
+ */
+#ifndef ICRC_ORACLE_H
+#define ICRC_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes (mirror PacketProcessorError, packet_processor.rs:127-148). */
+#define ORACLE_OK 0
+#define ORACLE_EINVAL (-22)            /* reference panics (short buffer)           */
+#define ORACLE_BUFFER_NOT_LARGE (-1000) /* BufferNotLargeEnough(usize)              */
+#define ORACLE_LENGTH_TOO_LONG (-1001)  /* LengthTooLong(usize)                     */
+#define ORACLE_INVALID_METADATA (-1002) /* PacketError::InvalidMetadataType          */
+#define ORACLE_INVALID_OPCODE (-1003)   /* PacketError::InvalidOpcode                */
+
+/* Opcodes: ToHostWorkRbDescOpcode (third_party/queues.rs:393-425). */
+enum {
+    OP_WRITE_FIRST = 0x06,
+    OP_WRITE_MIDDLE = 0x07,
+    OP_WRITE_LAST = 0x08,
+    OP_WRITE_LAST_IMM = 0x09,
+    OP_WRITE_ONLY = 0x0a,
+    OP_WRITE_ONLY_IMM = 0x0b,
+    OP_READ_REQUEST = 0x0c,
+    OP_READ_RESP_FIRST = 0x0d,
+    OP_READ_RESP_MIDDLE = 0x0e,
+    OP_READ_RESP_LAST = 0x0f,
+    OP_READ_RESP_ONLY = 0x10,
+    OP_ACK = 0x11,
+};
+
+/* A flattened RdmaMessage (types.rs RdmaMessage / Metadata / PayloadInfo). */
+typedef struct oracle_rdma_msg {
+    uint8_t kind; /* 0 = Metadata::General, 1 = Metadata::Acknowledge */
+    uint8_t opcode;
+    uint8_t tran_type; /* ToHostWorkRbDescTransType, RC = 0 */
+    uint8_t solicited;
+    uint8_t ack_req;
+    uint8_t aeth_code;
+    uint8_t aeth_value;
+    uint8_t has_imm;
+    uint8_t has_secondary_reth;
+    uint8_t _pad0[3];
+    uint16_t pkey;
+    uint16_t _pad1;
+    uint32_t dqpn;
+    uint32_t psn;
+    uint32_t msn;
+    uint32_t imm;
+    uint64_t reth_va;
+    uint32_t reth_rkey;
+    uint32_t reth_len;
+    uint64_t sec_va;
+    uint32_t sec_rkey;
+    uint32_t sec_len;
+    const uint8_t *payload; /* one SG element */
+    uint64_t payload_len;
+} oracle_rdma_msg;
+
+/* --- CRC core (crc32fast::Hasher semantics: zlib-style chaining) --------------------- */
+uint32_t oracle_crc32(uint32_t crc, const uint8_t *p, size_t n);
+
+/* --- ICRC (packet_processor.rs:268-353) --------------------------------------------- */
+int oracle_compute_icrc(const uint8_t *pkt, size_t len, uint32_t *out);
+int oracle_is_icrc_valid(uint8_t *pkt, size_t len, int *ok);
+/* Batch helpers used by tests / cpu_baseline: (offset,len) arrays. */
+int oracle_compute_icrc_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len,
+                              uint64_t n, uint32_t *out);
+
+/* --- Packet synthesis (packet_processor.rs:150-265,303-332; packet.rs:100-243) ------- */
+void oracle_write_ip_udp_header(uint8_t *buf, uint32_t src_ip, uint16_t src_port, uint32_t dst_ip,
+                                uint16_t dst_port, uint16_t total_length, uint16_t ip_id);
+int oracle_header_len(uint8_t opcode);
+int oracle_packet_write(uint8_t *buf, size_t buf_len, const oracle_rdma_msg *msg, uint32_t src_ip,
+                        uint16_t src_port, uint32_t dst_ip, uint16_t dst_port, uint16_t ip_id,
+                        size_t *out_len);
+uint32_t oracle_pad_cnt(uint64_t payload_len);
+
+/* net/util.rs:134-170: returns the 20-byte UDP payload of the 48-byte ACK packet. */
+int oracle_generate_ack(uint16_t pkey, uint32_t peer_qpn, uint32_t expected_psn, uint8_t *pkt48,
+                        uint8_t *udp_payload20);
+
+/* common.rs:152-176 */
+uint32_t oracle_generate_segments(uint64_t va, uint32_t len, uint32_t path_mtu, uint64_t *seg_va,
+                                  uint32_t *seg_len, uint32_t max_segs);
+
+/* responser.rs:321-338 (IPv4 header checksum, §8f row 4). */
+uint16_t oracle_ipv4_checksum(const uint8_t *hdr20);
+
+/* --- Synthetic workloads ----------------------------------------------- */
+uint64_t oracle_mix64(uint64_t x);
+/* Emulator WRITE send path (write.rs:31-96 + common.rs:73-132 + util.rs:172-186):
+ * one RDMA WRITE of `total_len` bytes from local `local_va` to `remote_va`, segmented at
+ * `pmtu`; every packet written (full IPv4 packet incl. ICRC) at base + i*stride.
+ * payload byte q of the message = byte (q & 7) of oracle_mix64(payload_key + (q >> 3))
+ * (payload_key == UINT64_MAX: the `i as u8` pattern of common.rs:240).
+ * Returns the number of packets, fills lens[] (L per packet). */
+int64_t oracle_synth_write(uint8_t *base, uint64_t stride, uint64_t max_pkts, uint32_t *lens,
+                           uint64_t local_va, uint64_t remote_va, uint32_t total_len,
+                           uint32_t pmtu, uint32_t rkey, uint32_t dqpn, uint32_t psn0,
+                           uint16_t msn, uint32_t dst_ip, uint64_t payload_key);
+
+/* A stream of `n` WRITE_MIDDLE packets of one QP: packet p carries
+ * message bytes [p*pmtu, (p+1)*pmtu), psn = psn0 + p, RETH va = remote_va + p*pmtu,
+ * RETH len = reth_len; other fields as oracle_synth_write. */
+int64_t oracle_synth_middle_stream(uint8_t *base, uint64_t stride, uint64_t n, uint32_t *lens,
+                                   uint64_t remote_va, uint32_t reth_len, uint32_t pmtu,
+                                   uint32_t rkey, uint32_t dqpn, uint32_t psn0, uint16_t msn,
+                                   uint32_t dst_ip, uint64_t payload_key);
+
+/* --- CPU baseline (icrc_fast.c): crc32fast-equivalent PCLMULQDQ folding core ---------- */
+uint32_t fast_crc32_slice16(uint32_t crc, const uint8_t *p, size_t n);
+uint32_t fast_crc32(uint32_t crc, const uint8_t *p, size_t n); /* pclmul when >= 128 B */
+int fast_compute_icrc(const uint8_t *pkt, size_t len, uint32_t *out);
+/* Time-bounded batch: ICRC of packets base + i*stride (len each) for i in [0,n), using
+ * `threads` POSIX threads; returns elapsed seconds, writes out[]. */
+double fast_icrc_strided_timed(const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
+                               uint32_t *out, int threads);
+/* The emulator send-path cost model (util.rs:172-186): per packet an 8 KiB vec![0; 8192]
+ * + payload copy in + ICRC + UDP-payload copy out (to_vec). Returns elapsed seconds. */
+double fast_emulator_path_timed(const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
+                                uint32_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

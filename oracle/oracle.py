@@ -1,0 +1,283 @@
+"""oracle.py — TEST INFRASTRUCTURE ONLY: ctypes loader for the CPU restatement.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module,
+and only as the checker.  The product path (open-rdma-driver_amd/) never imports it.
+
+Every wrapped function restates the reference ICRC path; see icrc_oracle.c for the
+file:line each one follows (packet_processor.rs:268-353 for compute/verify).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+
+OK = 0
+EINVAL = -22
+BUFFER_NOT_LARGE = -1000
+LENGTH_TOO_LONG = -1001
+INVALID_METADATA = -1002
+INVALID_OPCODE = -1003
+
+OP_WRITE_FIRST = 0x06
+OP_WRITE_MIDDLE = 0x07
+OP_WRITE_LAST = 0x08
+OP_WRITE_LAST_IMM = 0x09
+OP_WRITE_ONLY = 0x0A
+OP_WRITE_ONLY_IMM = 0x0B
+OP_READ_REQUEST = 0x0C
+OP_READ_RESP_FIRST = 0x0D
+OP_READ_RESP_MIDDLE = 0x0E
+OP_READ_RESP_LAST = 0x0F
+OP_READ_RESP_ONLY = 0x10
+OP_ACK = 0x11
+
+
+class RdmaMsg(ctypes.Structure):
+    """Flattened RdmaMessage (types.rs); layout == oracle_rdma_msg in icrc_oracle.h."""
+
+    _fields_ = [
+        ("kind", ctypes.c_uint8),
+        ("opcode", ctypes.c_uint8),
+        ("tran_type", ctypes.c_uint8),
+        ("solicited", ctypes.c_uint8),
+        ("ack_req", ctypes.c_uint8),
+        ("aeth_code", ctypes.c_uint8),
+        ("aeth_value", ctypes.c_uint8),
+        ("has_imm", ctypes.c_uint8),
+        ("has_secondary_reth", ctypes.c_uint8),
+        ("_pad0", ctypes.c_uint8 * 3),
+        ("pkey", ctypes.c_uint16),
+        ("_pad1", ctypes.c_uint16),
+        ("dqpn", ctypes.c_uint32),
+        ("psn", ctypes.c_uint32),
+        ("msn", ctypes.c_uint32),
+        ("imm", ctypes.c_uint32),
+        ("reth_va", ctypes.c_uint64),
+        ("reth_rkey", ctypes.c_uint32),
+        ("reth_len", ctypes.c_uint32),
+        ("sec_va", ctypes.c_uint64),
+        ("sec_rkey", ctypes.c_uint32),
+        ("sec_len", ctypes.c_uint32),
+        ("payload", ctypes.c_void_p),
+        ("payload_len", ctypes.c_uint64),
+    ]
+
+
+def build() -> str:
+    """Compile the oracle library (gcc) if needed; returns its path."""
+    srcs = [os.path.join(_HERE, f) for f in ("icrc_oracle.c", "icrc_fast.c", "icrc_oracle.h")]
+    if not os.path.exists(_LIB_PATH) or any(
+        os.path.getmtime(s) > os.path.getmtime(_LIB_PATH) for s in srcs
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.c_void_p
+        L.oracle_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.oracle_crc32.restype = ctypes.c_uint32
+        L.oracle_compute_icrc.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_compute_icrc.restype = ctypes.c_int
+        L.oracle_is_icrc_valid.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_is_icrc_valid.restype = ctypes.c_int
+        L.oracle_compute_icrc_batch.argtypes = [u8p, u8p, u8p, ctypes.c_uint64, u8p]
+        L.oracle_compute_icrc_batch.restype = ctypes.c_int
+        L.oracle_packet_write.argtypes = [
+            u8p, ctypes.c_size_t, ctypes.POINTER(RdmaMsg), ctypes.c_uint32, ctypes.c_uint16,
+            ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint16, ctypes.POINTER(ctypes.c_size_t),
+        ]
+        L.oracle_packet_write.restype = ctypes.c_int
+        L.oracle_generate_ack.argtypes = [ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32, u8p, u8p]
+        L.oracle_generate_ack.restype = ctypes.c_int
+        L.oracle_generate_segments.argtypes = [
+            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u8p, u8p, ctypes.c_uint32,
+        ]
+        L.oracle_generate_segments.restype = ctypes.c_uint32
+        L.oracle_ipv4_checksum.argtypes = [u8p]
+        L.oracle_ipv4_checksum.restype = ctypes.c_uint16
+        L.oracle_mix64.argtypes = [ctypes.c_uint64]
+        L.oracle_mix64.restype = ctypes.c_uint64
+        L.oracle_header_len.argtypes = [ctypes.c_uint8]
+        L.oracle_header_len.restype = ctypes.c_int
+        L.oracle_synth_write.argtypes = [
+            u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.c_uint64,
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64,
+        ]
+        L.oracle_synth_write.restype = ctypes.c_int64
+        L.oracle_synth_middle_stream.argtypes = [
+            u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.c_uint32,
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
+            ctypes.c_uint32, ctypes.c_uint64,
+        ]
+        L.oracle_synth_middle_stream.restype = ctypes.c_int64
+        L.fast_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.fast_crc32.restype = ctypes.c_uint32
+        L.fast_crc32_slice16.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.fast_crc32_slice16.restype = ctypes.c_uint32
+        L.fast_compute_icrc.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]
+        L.fast_compute_icrc.restype = ctypes.c_int
+        L.fast_icrc_strided_timed.argtypes = [
+            u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p, ctypes.c_int,
+        ]
+        L.fast_icrc_strided_timed.restype = ctypes.c_double
+        L.fast_emulator_path_timed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p]
+        L.fast_emulator_path_timed.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _as_u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def crc32(data, crc: int = 0) -> int:
+    a = _as_u8(data)
+    return lib().oracle_crc32(crc, _ptr(a), a.size)
+
+
+def compute_icrc(pkt) -> int:
+    """compute_icrc (packet_processor.rs:275-301). Raises ValueError where the reference panics."""
+    a = _as_u8(pkt)
+    out = ctypes.c_uint32()
+    rc = lib().oracle_compute_icrc(_ptr(a), a.size, ctypes.byref(out))
+    if rc:
+        raise ValueError(f"compute_icrc: rc={rc}")
+    return out.value
+
+
+def is_icrc_valid(pkt: np.ndarray) -> bool:
+    """is_icrc_valid (packet_processor.rs:341-353); zeroes the trailer of `pkt` in place."""
+    assert isinstance(pkt, np.ndarray) and pkt.dtype == np.uint8 and pkt.flags.c_contiguous
+    ok = ctypes.c_int()
+    rc = lib().oracle_is_icrc_valid(_ptr(pkt), pkt.size, ctypes.byref(ok))
+    if rc:
+        raise ValueError(f"is_icrc_valid: rc={rc}")
+    return bool(ok.value)
+
+
+def compute_icrc_batch(base: np.ndarray, off: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    out = np.zeros(off.size, dtype=np.uint32)
+    rc = lib().oracle_compute_icrc_batch(_ptr(base), _ptr(off), _ptr(lens), off.size, _ptr(out))
+    if rc:
+        raise ValueError(f"compute_icrc_batch: rc={rc}")
+    return out
+
+
+def packet_write(msg: RdmaMsg, src_ip: int, src_port: int, dst_ip: int, dst_port: int,
+                 ip_id: int, buf_len: int = 8192):
+    """PacketWriter::write (packet_processor.rs:210-265) into a zeroed buffer.
+    Returns (rc, packet bytes as np.uint8 array of length L, or None)."""
+    buf = np.zeros(buf_len, dtype=np.uint8)
+    n = ctypes.c_size_t()
+    rc = lib().oracle_packet_write(_ptr(buf), buf_len, ctypes.byref(msg), src_ip, src_port,
+                                   dst_ip, dst_port, ip_id, ctypes.byref(n))
+    if rc:
+        return rc, None
+    return rc, buf[: n.value].copy()
+
+
+def generate_ack(pkey: int, peer_qpn: int, expected_psn: int):
+    pkt = np.zeros(48, dtype=np.uint8)
+    udp = np.zeros(20, dtype=np.uint8)
+    rc = lib().oracle_generate_ack(pkey, peer_qpn, expected_psn, _ptr(pkt), _ptr(udp))
+    if rc:
+        raise ValueError(f"generate_ack: rc={rc}")
+    return pkt, udp
+
+
+def generate_segments(va: int, length: int, pmtu: int):
+    n = lib().oracle_generate_segments(va, length, pmtu, None, None, 0)
+    sva = np.zeros(n, dtype=np.uint64)
+    sl = np.zeros(n, dtype=np.uint32)
+    lib().oracle_generate_segments(va, length, pmtu, _ptr(sva), _ptr(sl), n)
+    return [(int(a), int(b)) for a, b in zip(sva, sl)]
+
+
+def ipv4_checksum(hdr) -> int:
+    a = _as_u8(hdr)
+    return lib().oracle_ipv4_checksum(_ptr(a))
+
+
+def mix64(x: int) -> int:
+    return lib().oracle_mix64(x & 0xFFFFFFFFFFFFFFFF)
+
+
+def synth_write(total_len: int, pmtu: int, *, local_va: int, remote_va: int, rkey: int,
+                dqpn: int, psn0: int, msn: int, dst_ip: int, payload_key: int,
+                stride: int | None = None):
+    """Emulator WRITE send path; returns (buffer, offsets, lens)."""
+    n = len(generate_segments(local_va, total_len, pmtu))
+    stride = stride or ((28 + 28 + pmtu + 4 + 3) // 4 * 4)
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint32)
+    got = lib().oracle_synth_write(_ptr(buf), stride, n, _ptr(lens), local_va, remote_va,
+                                   total_len, pmtu, rkey, dqpn, psn0, msn, dst_ip, payload_key)
+    if got != n:
+        raise ValueError(f"synth_write: rc={got}")
+    off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    return buf, off, lens
+
+
+def synth_middle_stream(n: int, *, pmtu: int = 4096, stride: int | None = None,
+                        remote_va: int = 0x7F7E8FC00000, reth_len: int = 0, rkey: int = 0x2000003,
+                        dqpn: int = 2, psn0: int = 0, msn: int = 0, dst_ip: int = 0xC0A80003,
+                        payload_key: int = 0x5EED):
+    stride = stride or (28 + 28 + pmtu + 4)
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint32)
+    got = lib().oracle_synth_middle_stream(_ptr(buf), stride, n, _ptr(lens), remote_va, reth_len,
+                                           pmtu, rkey, dqpn, psn0, msn, dst_ip, payload_key)
+    if got != n:
+        raise ValueError(f"synth_middle_stream: rc={got}")
+    off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    return buf, off, lens
+
+
+def fast_crc32(data, crc: int = 0) -> int:
+    a = _as_u8(data)
+    return lib().fast_crc32(crc, _ptr(a), a.size)
+
+
+def fast_compute_icrc(pkt) -> int:
+    a = _as_u8(pkt)
+    out = ctypes.c_uint32()
+    rc = lib().fast_compute_icrc(_ptr(a), a.size, ctypes.byref(out))
+    if rc:
+        raise ValueError(f"fast_compute_icrc: rc={rc}")
+    return out.value
+
+
+def fast_icrc_strided_timed(base: np.ndarray, stride: int, length: int, n: int, threads: int = 1):
+    out = np.zeros(n, dtype=np.uint32)
+    secs = lib().fast_icrc_strided_timed(_ptr(base), stride, length, n, _ptr(out), threads)
+    return secs, out
+
+
+def fast_emulator_path_timed(base: np.ndarray, stride: int, length: int, n: int):
+    out = np.zeros(n, dtype=np.uint32)
+    secs = lib().fast_emulator_path_timed(_ptr(base), stride, length, n, _ptr(out))
+    return secs, out

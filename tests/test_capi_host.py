@@ -1,0 +1,191 @@
+"""CPU suite: the product library loads, exports every symbol include/icrc.h declares, its
+host-side logic (headers, workloads, table image) is right, and the HIP algorithm — emulated
+on the CPU with the product's own table image — equals the oracle.  No compute call is made
+without a GPU; with no GPU, compute calls must fail loudly (ENODEV), never fall back."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import kernel_emu
+from golden_kats import KATS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "icrc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^[a-z_][\w \*]*?\b(icrc_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    import icrc_amd
+
+    names = declared_functions()
+    assert len(names) == 22, names
+    missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
+    assert not missing, missing
+
+
+def test_library_is_gfx950_hip_code():
+    import icrc_amd
+
+    blob = open(icrc_amd.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"icrc_batch_kernel" in blob
+
+
+def test_no_gpu_means_loud_failure():
+    import icrc_amd
+
+    if icrc_amd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(icrc_amd.IcrcError) as e:
+        icrc_amd.compute_icrc(bytes(64))
+    assert e.value.rc == icrc_amd.ENODEV
+    with pytest.raises(icrc_amd.IcrcError):
+        icrc_amd.Engine(0)
+
+
+def test_bad_arguments_rejected_before_device():
+    import icrc_amd
+
+    with pytest.raises(icrc_amd.IcrcError) as e:
+        icrc_amd.compute_icrc(bytes(43))
+    assert e.value.rc == icrc_amd.EINVAL
+    with pytest.raises(icrc_amd.IcrcError) as e:
+        icrc_amd.compute_icrc_batch(np.zeros(100, np.uint8), [0], [10])
+    assert e.value.rc == icrc_amd.EINVAL
+
+
+def test_table_image_against_gf2_definition():
+    import icrc_amd
+
+    img = icrc_amd.table_image()
+
+    def advance_words(s, n):
+        for _ in range(4 * n):
+            s = (s >> 8) ^ oracle_table[s & 0xFF]
+        return s
+
+    oracle_table = []
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ 0xEDB88320 if c & 1 else c >> 1
+        oracle_table.append(c)
+    rng = np.random.default_rng(0)
+    for _ in range(40):
+        b, x, copy = int(rng.integers(4)), int(rng.integers(256)), int(rng.integers(32))
+        addr = (b >> 1) * 65536 + x * 256 + (b & 1) * 128 + copy * 4
+        assert img[addr // 4] == advance_words(x << (8 * b), 64)
+    for _ in range(40):
+        lane, n, v = int(rng.integers(64)), int(rng.integers(8)), int(rng.integers(16))
+        addr = 131072 + (n * 16 + v) * 256 + lane * 4
+        assert img[addr // 4] == advance_words(v << (4 * n), 64 - lane)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_kernel_algorithm_emulation_matches_oracle(seed):
+    import icrc_amd
+
+    img = icrc_amd.table_image()
+    rng = np.random.default_rng(seed)
+    lengths = [44, 45, 46, 47, 48, 60, 255, 256, 257, 258, 259, 300, 1084, 4156, 4157, 4158, 4159]
+    for L in lengths + [int(x) for x in rng.integers(44, 3000, 10)]:
+        p = rng.integers(0, 256, L, dtype=np.uint8)
+        assert kernel_emu.icrc(img, p) == oracle.compute_icrc(p), L
+    for pkt, want in KATS:
+        assert kernel_emu.icrc(img, np.frombuffer(pkt, np.uint8)) == want
+
+
+def test_header_writer_matches_oracle_packet_writer():
+    import icrc_amd
+
+    for opcode in (0x06, 0x07, 0x08, 0x09, 0x0A, 0x0B, 0x0C, 0x0D, 0x10, 0x11):
+        for plen in (0, 3, 4096):
+            m1, m2 = icrc_amd.RdmaMsg(), oracle.RdmaMsg()
+            payload = np.arange(max(plen, 1), dtype=np.uint8)
+            for m in (m1, m2):
+                m.kind = 1 if opcode == 0x11 else 0
+                m.opcode = opcode
+                m.ack_req = opcode in (0x08, 0x0A)
+                m.solicited = 0
+                m.pkey = 7
+                m.dqpn = 0x55
+                m.psn = 0xFFFFFF
+                m.msn = 3
+                m.aeth_value = 0x1F
+                m.reth_va = 0xDEADBEEF0000
+                m.reth_rkey = 9
+                m.reth_len = 1 << 24
+                m.has_imm = 1
+                m.imm = 0xAA55
+                m.has_secondary_reth = 1
+                m.sec_va = 1
+                m.payload = payload.ctypes.data
+                m.payload_len = plen
+            hdr, total = icrc_amd.packet_headers(m1, "192.168.0.2", 4791, "192.168.0.3", 4791, 1)
+            rc, ref = oracle.packet_write(m2, 0xC0A80002, 4791, 0xC0A80003, 4791, 1)
+            assert rc == 0 and ref.size == total
+            np.testing.assert_array_equal(hdr, ref[: hdr.size])
+
+
+def _expand_on_host(w, icrc_amd):
+    """CPU model of icrc_synth_kernel for a few packets (test helper)."""
+    out = np.zeros(w.total_bytes, np.uint8)
+    for i in range(w.n):
+        d = w.desc[i]
+        o, hl, pl, tl = int(d["offset"]), int(d["hdr_len"]), int(d["payload_len"]), int(d["total_len"])
+        out[o: o + hl] = w.hdr[int(d["hdr_index"]), :hl]
+        for q in range(pl):
+            pos = int(d["payload_pos"]) + q
+            out[o + hl + q] = (oracle.mix64(int(d["payload_key"]) + (pos >> 3)) >> (8 * (pos & 7))) & 0xFF
+    return out
+
+
+def test_workload_c1_headers_match_oracle_stream():
+    import icrc_amd
+
+    n = 8
+    w = icrc_amd.workloads.write_middle_stream(n, 256, reth_len=0)
+    host = _expand_on_host(w, icrc_amd)
+    ref, off, lens = oracle.synth_middle_stream(n, pmtu=256, payload_key=0x5EED5EED, reth_len=0)
+    assert lens.tolist() == w.lens.tolist()
+    for i in range(n):
+        a = host[int(w.off[i]): int(w.off[i]) + int(w.lens[i]) - 4]
+        b = ref[int(off[i]): int(off[i]) + int(lens[i]) - 4]
+        np.testing.assert_array_equal(a, b)
+
+
+def test_workload_c3_matches_oracle_write_path():
+    import icrc_amd
+
+    w = icrc_amd.workloads.write_message(20000, 4096, local_va=0x7F7E8EE00100)
+    host = _expand_on_host(w, icrc_amd)
+    ref, off, lens = oracle.synth_write(20000, 4096, local_va=0x7F7E8EE00100, remote_va=0x7F7E8FC00000,
+                                        rkey=0x2000003, dqpn=2, psn0=0, msn=0, dst_ip=0xC0A80003,
+                                        payload_key=0xABCDEF)
+    assert lens.tolist() == w.lens.tolist()
+    for i in range(w.n):
+        a = host[int(w.off[i]): int(w.off[i]) + int(w.lens[i]) - 4]
+        b = ref[int(off[i]): int(off[i]) + int(lens[i]) - 4]
+        np.testing.assert_array_equal(a, b)
+
+
+def test_workload_c2_mixed_shape():
+    import icrc_amd
+
+    w = icrc_amd.workloads.mixed_mtu_stream(50000)
+    pl = w.desc["payload_len"]
+    assert set(np.unique(w.lens % 4).tolist()) == {0}
+    frac256 = float(np.mean(pl == 256))
+    assert 0.7 < frac256 < 0.85          # power-law k^-1.5 over {256, 1024, 4096}, 90 % full
+    assert 0.07 < float(np.mean(w.desc["payload_len"] % 4 != 0) + np.mean(
+        (pl != 256) & (pl != 1024) & (pl != 4096) & (pl % 4 == 0))) < 0.13
+    assert np.all(w.off[1:] >= w.off[:-1] + w.lens[:-1])
