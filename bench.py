@@ -103,10 +103,7 @@ def main() -> int:
     n = args.packets
     w = workloads.write_middle_stream(n, args.pmtu, dqpn=2 + rank, payload_key=0x5EED5EED + rank)
     L = int(w.lens[0])
-    d_buf = torch.empty(w.total_bytes, dtype=torch.uint8, device="cuda")
-    d_hdr, d_desc = dev(w.hdr), dev(w.desc.view(np.uint8))
-    eng.synth(d_buf.data_ptr(), d_desc.data_ptr(), d_hdr.data_ptr(), n, stream=stream)
-    del d_hdr, d_desc
+    d_buf = workloads.synthesize(eng, w, stream=stream)
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
 
@@ -200,8 +197,7 @@ def extra_measurements(eng, stream, args, world):
     n = args.packets
     w = workloads.write_middle_stream(n, args.pmtu)
     L = int(w.lens[0])
-    d_buf = torch.empty(w.total_bytes, dtype=torch.uint8, device="cuda")
-    eng.synth(d_buf.data_ptr(), dev(w.desc.view(np.uint8)).data_ptr(), dev(w.hdr).data_ptr(), n, stream=stream)
+    d_buf = workloads.synthesize(eng, w, stream=stream)
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
     eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), True, stream)
     d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -213,8 +209,7 @@ def extra_measurements(eng, stream, args, world):
 
     # mixed MTU
     wm = workloads.mixed_mtu_stream(4 << 20)
-    d_buf = torch.empty(wm.total_bytes, dtype=torch.uint8, device="cuda")
-    eng.synth(d_buf.data_ptr(), dev(wm.desc.view(np.uint8)).data_ptr(), dev(wm.hdr).data_ptr(), wm.n, stream=stream)
+    d_buf = workloads.synthesize(eng, wm, stream=stream)
     d_off, d_len = dev(wm.off), dev(wm.lens)
     d_out = torch.zeros(wm.n, dtype=torch.int32, device="cuda")
     wall, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n,
@@ -227,8 +222,7 @@ def extra_measurements(eng, stream, args, world):
 
     # 16 MiB WRITE round trip: compute(send, write trailer) + verify(recv)
     w3 = workloads.write_message(16 << 20, 4096)
-    d_buf = torch.empty(w3.total_bytes, dtype=torch.uint8, device="cuda")
-    eng.synth(d_buf.data_ptr(), dev(w3.desc.view(np.uint8)).data_ptr(), dev(w3.hdr).data_ptr(), w3.n, stream=stream)
+    d_buf = workloads.synthesize(eng, w3, stream=stream)
     d_off, d_len = dev(w3.off), dev(w3.lens)
     d_out = torch.zeros(w3.n, dtype=torch.int32, device="cuda")
     d_ok = torch.zeros(w3.n, dtype=torch.uint8, device="cuda")
@@ -248,8 +242,7 @@ def extra_measurements(eng, stream, args, world):
     nh = min(args.packets, 1 << 18)
     wh = workloads.write_middle_stream(nh, args.pmtu)
     Lh = int(wh.lens[0])
-    d_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, device="cuda")
-    eng.synth(d_buf.data_ptr(), dev(wh.desc.view(np.uint8)).data_ptr(), dev(wh.hdr).data_ptr(), nh, stream=stream)
+    d_buf = workloads.synthesize(eng, wh, stream=stream)
     h_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, pin_memory=True)
     h_buf.copy_(d_buf)
     h_out = torch.empty(nh, dtype=torch.int32, pin_memory=True)

@@ -15,7 +15,8 @@
  *       packet_processor.rs:150-265 (+ write_ip_udp_header 303-332)
  *
  * Plain pointers and sizes only; no HIP or torch types appear in the signatures (a HIP
- * stream is passed as an opaque `void*`, i.e. a hipStream_t; NULL = the engine's stream).
+ * stream is passed as an opaque `void*`, i.e. a hipStream_t; NULL = the HIP null stream, as in
+ * every HIP API; icrc_engine_stream() returns the engine's own non-blocking stream).
  *
  * Conventions
  *   - A packet is a full IPv4 datagram (no Ethernet header) starting at the IPv4 header;
@@ -67,6 +68,11 @@ int icrc_engine_destroy(icrc_engine *engine);
 /* Lazily created, lock-protected default engine for `device` (-1 = current HIP device). */
 int icrc_engine_default(int device, icrc_engine **out);
 int icrc_engine_device_ordinal(const icrc_engine *engine);
+/* The engine's own non-blocking stream (a hipStream_t), for callers without one. */
+void *icrc_engine_stream(const icrc_engine *engine);
+/* Tuning knob for A/B measurement: 0 = one packet per wavefront at a time, S >= 1 = software-
+ * pipelined with S packets in flight per wavefront; -1 = the default.  Results are identical. */
+int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
 int icrc_device_count(void);
 /* Static library/kernel description (for logs): "icrc_amd <ver> gfx950 ..." */

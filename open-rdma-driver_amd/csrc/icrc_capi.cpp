@@ -15,6 +15,7 @@
 struct icrc_engine {
     int device = 0;
     int num_cu = 0;
+    int variant = icrc::kDefaultVariant;
     uint32_t *d_table = nullptr;
     hipStream_t stream = nullptr;
     std::mutex mu;  // guards the staging buffers below
@@ -153,6 +154,7 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
         p.n = cnt;
         p.table = e->d_table;
         p.trailer = 0;  // trailers are written on the host copy below
+        p.variant = e->variant;
         if (mode == icrc::kCompute) p.out = e->d_res;
         else p.ok = reinterpret_cast<uint8_t *>(e->d_res);
         rc = icrc::launch_batch(mode, p, grid_for(e, cnt), e->stream);
@@ -204,7 +206,8 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     p.nerr = d_nerr;
     p.table = e->d_table;
     p.trailer = trailer ? 1 : 0;
-    return icrc::launch_batch(mode, p, grid_for(e, n), stream ? stream : e->stream);
+    p.variant = e->variant;
+    return icrc::launch_batch(mode, p, grid_for(e, n), stream);
 }
 
 }  // namespace
@@ -301,6 +304,14 @@ int icrc_engine_default(int device, icrc_engine **out) {
 
 int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : ICRC_EINVAL; }
 
+int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
+    if (!e || variant < -1 || variant > icrc::kMaxVariant) return ICRC_EINVAL;
+    e->variant = variant < 0 ? icrc::kDefaultVariant : variant;
+    return ICRC_OK;
+}
+
+void *icrc_engine_stream(const icrc_engine *e) { return e ? static_cast<void *>(e->stream) : nullptr; }
+
 uint32_t icrc_compute(const uint8_t *pkt, size_t len, int *err) {
     int dummy;
     int *rc = err ? err : &dummy;
@@ -393,7 +404,7 @@ int icrc_synth_device(icrc_engine *e, uint8_t *d_base, const icrc_synth_desc *d_
     if (!e || !d_base || !d_desc || !d_hdr) return ICRC_EINVAL;
     DeviceGuard g(e->device);
     if (!g.ok) return ICRC_ENODEV;
-    return icrc::launch_synth(d_base, d_desc, d_hdr, n, stream ? stream : e->stream);
+    return icrc::launch_synth(d_base, d_desc, d_hdr, n, stream);
 }
 
 // Host-only helper for tests: the LDS table image (no GPU needed).

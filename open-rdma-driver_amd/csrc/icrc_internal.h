@@ -35,7 +35,11 @@ struct BatchParams {
     uint32_t *nerr;  // may be null
     const uint32_t *table;  // kLdsWords image in device memory
     int trailer;     // compute: write trailer; verify: zero trailer
+    int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
 };
+
+constexpr int kDefaultVariant = 3;
+constexpr int kMaxVariant = 7;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

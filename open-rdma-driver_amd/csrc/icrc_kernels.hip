@@ -31,7 +31,7 @@
 namespace icrc {
 namespace {
 
-constexpr int kGroup = 16;  // rows (each 256 B per wave) whose loads are issued together
+constexpr int kGroup = 8;  // long-packet path: rows (256 B per wave each) loaded together
 
 __device__ __forceinline__ uint32_t lds_at(const char *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
@@ -148,7 +148,275 @@ __device__ __forceinline__ uint32_t slow_packet_state(const char *lds, const uin
     return acc;
 }
 
+// Epilogue: store the ICRC (compute) or compare it with the trailer (verify), lane 0 only.
 template <int MODE>
+__device__ __forceinline__ void finish_packet(const BatchParams &p, uint32_t i, uint8_t *pkt, uint32_t Ld,
+                                              uint32_t crc, bool aligned, uint32_t lane) {
+    if (lane != 0) return;
+    uint8_t *tr = pkt + Ld;
+    if (MODE == kCompute) {
+        if (p.out) p.out[i] = crc;
+        if (p.trailer) {
+            if (aligned) {
+                *reinterpret_cast<uint32_t *>(tr) = crc;
+            } else {
+                tr[0] = static_cast<uint8_t>(crc);
+                tr[1] = static_cast<uint8_t>(crc >> 8);
+                tr[2] = static_cast<uint8_t>(crc >> 16);
+                tr[3] = static_cast<uint8_t>(crc >> 24);
+            }
+        }
+    } else {
+        uint32_t stored;
+        if (aligned) {
+            stored = *reinterpret_cast<const uint32_t *>(tr);
+        } else {
+            stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                     (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+        }
+        p.ok[i] = (stored == crc) ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+        if (p.trailer) {
+            if (aligned) {
+                *reinterpret_cast<uint32_t *>(tr) = 0u;
+            } else {
+                tr[0] = tr[1] = tr[2] = tr[3] = 0;
+            }
+        }
+    }
+}
+
+// One packet, any length/alignment, no pipelining (variant 0, and irregular packets).
+template <int MODE>
+__device__ __forceinline__ void handle_packet(const BatchParams &p, uint32_t i, const char *lds,
+                                           const LaneConsts &c, uint32_t lane) {
+    const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
+    const uint32_t L = p.len ? p.len[i] : p.ulen;
+    uint8_t *pkt = p.base + off;
+    if (L < ICRC_MIN_PACKET) {
+        if (lane == 0) {
+            if (p.nerr) atomicAdd(p.nerr, 1u);
+            if (MODE == kCompute) {
+                if (p.out) p.out[i] = 0u;
+            } else {
+                p.ok[i] = ICRC_VERIFY_BADLEN;
+            }
+        }
+        return;
+    }
+    const uint32_t Ld = L - 4u;
+    const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
+    const uint32_t acc = fast ? fast_packet_state(lds, pkt, Ld, c, lane) : slow_packet_state(lds, pkt, Ld, c, lane);
+    finish_packet<MODE>(p, i, pkt, Ld, ~wave_xor(final_mul(lds, acc, c.fin)), fast, lane);
+}
+
+// ---- pipelined path -----------------------------------------------------------------------
+// A wave walks its packets q = 0, 1, 2, ... (packet index first + q * tw) in sets of S
+// packets processed together (S independent CRC chains for ILP); the loads of set t + D are
+// issued before set t is processed (a D-deep register ring), so each wave keeps ~D*S packets
+// (~4 KiB each) in flight against the ~3 us loaded HBM latency.
+constexpr int kRows = 17;  // rows held in registers per packet: L <= 4352 (every MTU <= 4096)
+
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+// Compile-time unrolled loop: f(IntC<0>), f(IntC<1>), ... while f returns true.
+template <int N, int I = 0, class F>
+__device__ __forceinline__ bool static_for(F &&f) {
+    if constexpr (I < N) {
+        if (!f(IntC<I>{})) return false;
+        return static_for<N, I + 1>(f);
+    } else {
+        return true;
+    }
+}
+
+struct SlotMeta {
+    uint8_t *pkt;
+    uint32_t L;
+    uint32_t idx;
+    int R;      // rows (regular packets)
+    int k0;     // stream index of lane 0 in row 0
+    int kind;   // 0 = no packet, 1 = regular (aligned, 44 <= L, R <= kRows), 2 = irregular
+};
+
+// Ragged batches: (offset, len) of 64 consecutive packets of this wave's sequence, one per
+// lane, fetched with one vector load each and read back with v_readlane (uniform index).
+struct MetaBlock {
+    uint32_t off_lo, off_hi, len;  // per lane
+    int block;                     // uniform
+};
+
+__device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, uint32_t first, uint32_t tw,
+                                           int block, uint32_t lane) {
+    const uint64_t i = static_cast<uint64_t>(first) + (static_cast<uint64_t>(block) * 64u + lane) * tw;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (i < p.n) {
+        off = p.off ? p.off[i] : i * p.stride;
+        len = p.len ? p.len[i] : p.ulen;
+    }
+    mb.off_lo = static_cast<uint32_t>(off);
+    mb.off_hi = static_cast<uint32_t>(off >> 32);
+    mb.len = len;
+    mb.block = block;
+}
+
+__device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t first,
+                                          uint32_t tw, uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
+    m.kind = 0;
+    m.R = 0;
+    m.k0 = 0;
+    m.pkt = p.base;
+    m.L = 0;
+    m.idx = first + q * tw;
+    if (q >= nq) return;
+    uint64_t off;
+    uint32_t L;
+    if (ragged) {
+        const int block = static_cast<int>(q >> 6);
+        if (block != mb.block) meta_fetch(p, mb, first, tw, block, lane);
+        const int l = static_cast<int>(q & 63u);
+        off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
+              (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
+        L = __builtin_amdgcn_readlane(mb.len, l);
+    } else {
+        off = static_cast<uint64_t>(m.idx) * p.stride;
+        L = p.ulen;
+    }
+    m.pkt = p.base + off;
+    m.L = L;
+    m.kind = 2;
+    if (L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(m.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+        const int N = 1 + static_cast<int>((L - 4u) >> 2);
+        const int R = (N + 63) >> 6;
+        if (R <= kRows) {
+            m.kind = 1;
+            m.R = R;
+            m.k0 = N - 64 * R;
+        }
+    }
+}
+
+// Loads in three blocks by row count (short packets issue few instructions); rows past the
+// packet and every row of a non-regular slot read 0 through the descriptor's range check.
+template <int ABL>
+__device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[kRows]) {
+    if constexpr (ABL == 2) {
+#pragma unroll
+        for (int j = 0; j < kRows; ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
+        return;
+    }
+    const int nrec = m.kind == 1 ? static_cast<int>(m.L - 4u) : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
+    const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
+    if (m.R > 2) {
+#pragma unroll
+        for (int j = 2; j < 8; ++j)
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
+    }
+    if (m.R > 8) {
+#pragma unroll
+        for (int j = 8; j < kRows; ++j)
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
+    }
+}
+
+template <int MODE, int S, int ABL>
+__device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows]) {
+    int rmax = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (m[s].kind == 1 && m[s].R > rmax) rmax = m[s].R;
+    if (rmax > 0) {
+        uint32_t acc[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k = m[s].k0 + static_cast<int>(lane);
+            acc[s] = u[s][0] | head_mask(k);
+            u[s][1] |= head_mask(k + 64);
+        }
+        // One straight-line block per row for all S chains (the scheduler interleaves them);
+        // a chain past its own last row keeps its value through a select.
+#pragma unroll
+        for (int j = 1; j < kRows; ++j) {
+            if (j < rmax) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if constexpr (ABL == 1) {
+                        acc[s] ^= u[s][j];
+                    } else {
+                        const uint32_t t = mul_m64(lds, acc[s], c) ^ u[s][j];
+                        acc[s] = (j < m[s].R) ? t : acc[s];
+                    }
+                }
+            }
+        }
+        uint32_t fin[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (m[s].kind == 1) finish_packet<MODE>(p, m[s].idx, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (m[s].kind == 2) handle_packet<MODE>(p, m[s].idx, lds, c, lane);
+}
+
+template <int MODE, int S, int D, int ABL>
+__device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                              uint32_t lane, uint32_t first, uint32_t tw) {
+    constexpr int B = D + 1;
+    if (first >= p.n) return;
+    const uint32_t nq = (p.n - 1u - first) / tw + 1u;  // packets of this wave
+    const uint32_t nsets = (nq + S - 1) / S;
+    const bool ragged = p.off != nullptr || p.len != nullptr;
+    MetaBlock mb;
+    mb.block = -1;
+    mb.off_lo = mb.off_hi = mb.len = 0;
+    SlotMeta m[B][S];
+    uint32_t u[B][S][kRows];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (static_cast<uint32_t>(d) < nsets) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                slot_meta(p, mb, ragged, first, tw, d * S + s, nq, lane, m[d][s]);
+                slot_load<ABL>(m[d][s], lane, u[d][s]);
+            }
+        }
+    }
+    for (uint32_t t = 0; t < nsets; t += B) {
+        const bool cont = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            const uint32_t ts = t + b;
+            if (ts >= nsets) return false;
+            const uint32_t tp = ts + D;
+            if (tp < nsets) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    slot_meta(p, mb, ragged, first, tw, tp * S + s, nq, lane, m[bp][s]);
+                    slot_load<ABL>(m[bp][s], lane, u[bp][s]);
+                }
+            }
+            process_set<MODE, S, ABL>(p, lds, c, lane, m[b], u[b]);
+            return true;
+        });
+        if (!cont) return;
+    }
+}
+
+// Kernel variants (runtime-selected, identical results):
+//   0            one packet per wave at a time, no pipelining
+//   S, D, ABL    pipelined with S chains and a D-deep ring; ABL = 0 (real), 1 (loads only,
+//                no CRC: a memory-pipeline bound), 2 (CRC only, no loads: a compute bound).
+template <int MODE, int S, int D, int ABL>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -168,58 +436,11 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     c.fin = kFinalBase + lane * 4u;
 
     const uint32_t tw = gridDim.x * kWavesPerGroup;
-    for (uint32_t i = blockIdx.x * kWavesPerGroup + wave; i < p.n; i += tw) {
-        const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
-        const uint32_t L = p.len ? p.len[i] : p.ulen;
-        uint8_t *pkt = p.base + off;
-        if (L < ICRC_MIN_PACKET) {
-            if (lane == 0) {
-                if (p.nerr) atomicAdd(p.nerr, 1u);
-                if (MODE == kCompute) {
-                    if (p.out) p.out[i] = 0u;
-                } else {
-                    p.ok[i] = ICRC_VERIFY_BADLEN;
-                }
-            }
-            continue;
-        }
-        const uint32_t Ld = L - 4u;
-        const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
-        const uint32_t acc = fast ? fast_packet_state(lds, pkt, Ld, c, lane)
-                                  : slow_packet_state(lds, pkt, Ld, c, lane);
-        const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
-        if (lane == 0) {
-            uint8_t *tr = pkt + Ld;
-            if (MODE == kCompute) {
-                if (p.out) p.out[i] = crc;
-                if (p.trailer) {
-                    if (fast) {
-                        *reinterpret_cast<uint32_t *>(tr) = crc;
-                    } else {
-                        tr[0] = static_cast<uint8_t>(crc);
-                        tr[1] = static_cast<uint8_t>(crc >> 8);
-                        tr[2] = static_cast<uint8_t>(crc >> 16);
-                        tr[3] = static_cast<uint8_t>(crc >> 24);
-                    }
-                }
-            } else {
-                uint32_t stored;
-                if (fast) {
-                    stored = *reinterpret_cast<const uint32_t *>(tr);
-                } else {
-                    stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
-                             (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
-                }
-                p.ok[i] = (stored == crc) ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
-                if (p.trailer) {
-                    if (fast) {
-                        *reinterpret_cast<uint32_t *>(tr) = 0u;
-                    } else {
-                        tr[0] = tr[1] = tr[2] = tr[3] = 0;
-                    }
-                }
-            }
-        }
+    const uint32_t first = blockIdx.x * kWavesPerGroup + wave;
+    if constexpr (S == 0) {
+        for (uint32_t i = first; i < p.n; i += tw) handle_packet<MODE>(p, i, lds, c, lane);
+    } else {
+        run_pipelined<MODE, S, D, ABL>(p, lds, c, lane, first, tw);
     }
 }
 
@@ -276,13 +497,30 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 
 }  // namespace
 
+#define ICRC_LAUNCH(S, D, A) \
+    hipLaunchKernelGGL((icrc_batch_kernel<MODE, S, D, A>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+
+template <int MODE>
+static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
+    switch (p.variant) {
+    case 0: ICRC_LAUNCH(0, 1, 0); break;
+    case 1: ICRC_LAUNCH(1, 1, 0); break;
+    case 2: ICRC_LAUNCH(2, 1, 0); break;
+    case 3: ICRC_LAUNCH(1, 2, 0); break;
+    case 4: ICRC_LAUNCH(1, 3, 0); break;
+    case 5: ICRC_LAUNCH(2, 2, 0); break;
+    case 6: ICRC_LAUNCH(1, 2, 1); break;  // diagnostic: loads only
+    case 7: ICRC_LAUNCH(1, 2, 2); break;  // diagnostic: CRC only
+    default: ICRC_LAUNCH(1, 2, 0); break;
+    }
+}
+#undef ICRC_LAUNCH
+
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (mode == kCompute)
-        hipLaunchKernelGGL(icrc_batch_kernel<kCompute>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-    else
-        hipLaunchKernelGGL(icrc_batch_kernel<kVerify>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    if (mode == kCompute) launch_mode<kCompute>(p, grid, s);
+    else launch_mode<kVerify>(p, grid, s);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -101,6 +101,8 @@ def _load() -> ctypes.CDLL:
         "icrc_engine_destroy": (i32, [vp]),
         "icrc_engine_default": (i32, [i32, ctypes.POINTER(vp)]),
         "icrc_engine_device_ordinal": (i32, [vp]),
+        "icrc_engine_stream": (vp, [vp]),
+        "icrc_engine_set_kernel_variant": (i32, [vp, i32]),
         "icrc_device_count": (i32, []),
         "icrc_version": (ctypes.c_char_p, []),
         "icrc_compute": (u32, [vp, sz, ctypes.POINTER(i32)]),
@@ -280,13 +282,19 @@ def verify_icrc_batch(base: np.ndarray, off, lens, zero_trailer: bool = False) -
 class Engine:
     """One engine per GPU (icrc_engine_create).  Device entry points take raw device pointers
     (e.g. torch tensor .data_ptr()) and a hipStream_t handle (e.g.
-    torch.cuda.current_stream().cuda_stream); 0/None = the engine's own stream."""
+    torch.cuda.current_stream().cuda_stream); 0/None = the HIP null stream (torch's default
+    stream), engine.stream = the engine's own non-blocking stream."""
 
     def __init__(self, device: int = 0):
         h = ctypes.c_void_p()
         _check(lib.icrc_engine_create(device, ctypes.byref(h)), "icrc_engine_create")
         self.handle = h
         self.device = device
+        self.stream = lib.icrc_engine_stream(h) or 0
+
+    def set_variant(self, variant: int) -> None:
+        """Kernel variant for A/B runs (0 = unpipelined, S >= 1 = S packets in flight/wave)."""
+        _check(lib.icrc_engine_set_kernel_variant(self.handle, variant), "set_kernel_variant")
 
     def close(self) -> None:
         if self.handle:

@@ -51,6 +51,22 @@ class Workload:
         return int(self.desc["payload_len"].sum())
 
 
+def synthesize(engine, w: "Workload", d_buf=None, stream: int = 0, pad: int = 0):
+    """Expand workload `w` into packets in HBM with the device synthesiser (icrc_synth_device).
+    Returns the torch uint8 buffer.  The descriptor/header tensors are kept alive until the
+    stream has executed the kernel (the engine borrows device pointers until then)."""
+    import torch
+
+    if d_buf is None:
+        d_buf = torch.zeros(w.total_bytes + pad, dtype=torch.uint8, device="cuda")
+    d_desc = torch.from_numpy(np.ascontiguousarray(w.desc).view(np.uint8)).cuda()
+    d_hdr = torch.from_numpy(np.ascontiguousarray(w.hdr)).cuda()
+    engine.synth(d_buf.data_ptr(), d_desc.data_ptr(), d_hdr.data_ptr(), w.n, stream=stream)
+    torch.cuda.synchronize()
+    del d_desc, d_hdr
+    return d_buf
+
+
 def _pad_cnt(n):
     return (4 - (n % 4)) % 4
 

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""A/B the ICRC kernel variants in ONE process, interleaved rounds (methodology rule 24):
+C1 (1 Mi x 4156 B, strided) and C2 (mixed MTU, ragged) for each variant; checks that every
+variant returns identical ICRCs.  Prints one JSON line per (workload, variant)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "open-rdma-driver_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import icrc_amd  # noqa: E402
+from icrc_amd import workloads  # noqa: E402
+
+GIB = float(1 << 30)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def main():
+    variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2").split(",")]
+    rounds = int(os.environ.get("ROUNDS", "5"))
+    launches = int(os.environ.get("LAUNCHES", "10"))
+    eng = icrc_amd.Engine(0)
+    s = torch.cuda.current_stream().cuda_stream
+    w1 = workloads.write_middle_stream(1 << 20)
+    L = int(w1.lens[0])
+    b1 = workloads.synthesize(eng, w1, stream=s)
+    w2 = workloads.mixed_mtu_stream(4 << 20)
+    b2 = workloads.synthesize(eng, w2, stream=s)
+    o2, l2 = dev(w2.off), dev(w2.lens)
+    out1 = torch.zeros(w1.n, dtype=torch.int32, device="cuda")
+    out2 = torch.zeros(w2.n, dtype=torch.int32, device="cuda")
+    bytes1 = w1.n * L
+    bytes2 = int(w2.lens.astype(np.uint64).sum())
+    jobs = {
+        "C1": (lambda: eng.compute_strided(b1.data_ptr(), L, L, w1.n, out1.data_ptr(), False, s), bytes1, out1),
+        "C2": (lambda: eng.compute_batch(b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), w2.n, out2.data_ptr(),
+                                         False, 0, s), bytes2, out2),
+    }
+    times = {(j, v): [] for j in jobs for v in variants}
+    ref = {}
+    for r in range(rounds):
+        for v in variants:
+            eng.set_variant(v)
+            for j, (fn, nb, out) in jobs.items():
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(launches):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[(j, v)].append(e0.elapsed_time(e1) / launches)
+                got = out.cpu().numpy().copy()
+                if j not in ref:
+                    ref[j] = got
+                assert np.array_equal(ref[j], got), f"variant {v} differs on {j}"
+    for (j, v), ts in times.items():
+        nb = jobs[j][1]
+        med = float(np.median(ts))
+        print(json.dumps({"workload": j, "variant": v, "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                          "GB/s": round(nb / (med * 1e-3) / 1e9, 1), "frac_of_8TB": round(nb / (med * 1e-3) / 8e12, 4)}))
+    sys.stdout.flush()
+
+
+if __name__ == "__main__":
+    main()

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 22, names
+    assert len(names) == 24, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 

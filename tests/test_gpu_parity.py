@@ -86,6 +86,33 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_every_kernel_variant_is_bit_exact(engine, variant):
+    """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
+    misaligned and over-long packets and on a strided stream."""
+    rng = np.random.default_rng(100 + variant)
+    n = 1500
+    lens = rng.choice([44, 48, 316, 1084, 4156, 4157, 5000, 9000], n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 2, n - 1).astype(np.uint64) * 4
+                        + (rng.random(n - 1) < 0.05))
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    engine.set_variant(variant)
+    try:
+        out, nerr, _ = run_batch(engine, buf, off, lens)
+        assert nerr == 0
+        np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
+        sbuf, soff, slens = oracle.synth_middle_stream(777)
+        L = int(slens[0])
+        d = dev(sbuf)
+        d_out = torch.zeros(777, dtype=torch.int32, device="cuda")
+        engine.compute_strided(d.data_ptr(), L, L, 777, d_out.data_ptr(), stream=stream_handle())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), oracle_icrcs(sbuf, soff, slens))
+    finally:
+        engine.set_variant(-1)
+
+
 def test_max_and_boundary_lengths(engine):
     rng = np.random.default_rng(7)
     lens = np.array([44, 47, 48, 255, 256, 257, 259, 260, 1023, 1024, 1028, 4156, 4160, 8192,
@@ -169,9 +196,7 @@ def test_synth_c1_matches_oracle_bytes(engine):
 
     n = 256
     w = icrc_amd.workloads.write_middle_stream(n, reth_len=0)
-    d_buf = torch.zeros(w.total_bytes, dtype=torch.uint8, device="cuda")
-    engine.synth(d_buf.data_ptr(), dev(w.desc.view(np.uint8)).data_ptr(), dev(w.hdr).data_ptr(), n,
-                 stream=stream_handle())
+    d_buf = icrc_amd.workloads.synthesize(engine, w, stream=stream_handle())
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
     engine.compute_strided(d_buf.data_ptr(), w.stride, int(w.lens[0]), n, d_out.data_ptr(),
                            write_trailer=True, stream=stream_handle())
@@ -184,9 +209,7 @@ def test_mixed_mtu_stream(engine):
     import icrc_amd
 
     w = icrc_amd.workloads.mixed_mtu_stream(20000)
-    d_buf = torch.zeros(w.total_bytes, dtype=torch.uint8, device="cuda")
-    engine.synth(d_buf.data_ptr(), dev(w.desc.view(np.uint8)).data_ptr(), dev(w.hdr).data_ptr(),
-                 w.n, stream=stream_handle())
+    d_buf = icrc_amd.workloads.synthesize(engine, w, stream=stream_handle())
     out, nerr, host = run_batch(engine, d_buf.cpu().numpy(), w.off, w.lens)
     assert nerr == 0
     np.testing.assert_array_equal(out, oracle_icrcs(host, w.off, w.lens))
@@ -261,10 +284,8 @@ def test_full_size_c1_properties(engine, n):
 
     w = icrc_amd.workloads.write_middle_stream(n)
     L = int(w.lens[0])
-    d_buf = torch.empty(w.total_bytes, dtype=torch.uint8, device="cuda")
     s = stream_handle()
-    engine.synth(d_buf.data_ptr(), dev(w.desc.view(np.uint8)).data_ptr(), dev(w.hdr).data_ptr(), n,
-                 stream=s)
+    d_buf = icrc_amd.workloads.synthesize(engine, w, stream=s)
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
     engine.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), write_trailer=True, stream=s)
     d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
