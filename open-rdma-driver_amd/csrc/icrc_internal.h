@@ -38,8 +38,8 @@ struct BatchParams {
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
 };
 
-constexpr int kDefaultVariant = 3;
-constexpr int kMaxVariant = 7;
+constexpr int kDefaultVariant = 1;
+constexpr int kMaxVariant = 9;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

@@ -38,31 +38,50 @@ __device__ __forceinline__ uint32_t lds_at(const char *lds, uint32_t byte_addr) 
 }
 
 struct LaneConsts {
-    uint32_t lo0, lo1, lo2, lo3;  // bulk-table lane slots for bytes 0..3
-    uint32_t fin;                 // per-lane final-table base
+    // v_perm_b32 source: byte0 = this lane's bank slot (lane & 31) * 4 in the even tables,
+    // byte1 = the same slot + 128 in the odd tables, byte2 = 0x01 (the second 64 KiB region).
+    uint32_t pc;
+    uint32_t fin;  // per-lane final-table base
 };
 
-// M^64(s): four byte lookups (bytes are placed directly at address bits 8..15).
+// Table addresses of the four state bytes, one v_perm_b32 each: byte b of s lands in
+// address bits 8..15, the lane slot in bits 0..7, the region (b >> 1) in bit 16.
+constexpr uint32_t kSel0 = 0x0C0C0400u;  // [slot,   s.b0, 0,    0]
+constexpr uint32_t kSel1 = 0x0C0C0501u;  // [slot+128, s.b1, 0,  0]
+constexpr uint32_t kSel2 = 0x0C020600u;  // [slot,   s.b2, 0x01, 0]
+constexpr uint32_t kSel3 = 0x0C020701u;  // [slot+128, s.b3, 0x01, 0]
+
+// M^64(s) ^ u: four byte lookups; u is folded in before the last read arrives.
+__device__ __forceinline__ uint32_t step_m64(const char *lds, uint32_t s, uint32_t u, const LaneConsts &c) {
+    const uint32_t r0 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel0));
+    const uint32_t r1 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel1));
+    const uint32_t r2 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel2));
+    const uint32_t r3 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel3));
+    return ((r0 ^ r1) ^ (r2 ^ u)) ^ r3;
+}
+
 __device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const LaneConsts &c) {
-    const uint32_t a0 = ((s << 8) & 0xff00u) | c.lo0;
-    const uint32_t a1 = (s & 0xff00u) | c.lo1;
-    const uint32_t a2 = ((s >> 8) & 0xff00u) | c.lo2;
-    const uint32_t a3 = ((s >> 16) & 0xff00u) | c.lo3;
-    return lds_at(lds, a0) ^ lds_at(lds, a1) ^ lds_at(lds, a2) ^ lds_at(lds, a3);
+    return step_m64(lds, s, 0u, c);
 }
 
 // M^(64-lane)(acc) via 8 nibble lookups into this lane's private tables.
 __device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uint32_t fin) {
-    uint32_t r = 0;
+    uint32_t r[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) r ^= lds_at(lds, fin + n * 4096u + (((acc >> (4 * n)) & 15u) << 8));
-    return r;
+    for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, fin + n * 4096u + (((acc >> (4 * n)) & 15u) << 8));
+    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
 }
 
+// XOR over the 64 lanes with DPP (VALU, no LDS round trips): two quad permutes and two
+// row rotations leave every lane of each 16-lane row holding the row's XOR; the four row
+// values are combined on the scalar unit.  Returns a wave-uniform value.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) x ^= __shfl_xor(x, m, 64);
-    return x;
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x124, 0xF, 0xF, false));  // row_ror:4
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+    return __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 16) ^
+           __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
 }
 
 // Fast path (4-aligned packet, L % 4 == 0): OR-masks of the stream words that carry the
@@ -148,15 +167,14 @@ __device__ __forceinline__ uint32_t slow_packet_state(const char *lds, const uin
     return acc;
 }
 
-// Epilogue: store the ICRC (compute) or compare it with the trailer (verify), lane 0 only.
+// Epilogue of one packet: trailer handling (lane 0 stores) and the per-packet result —
+// compute: the ICRC; verify: ICRC_VERIFY_OK / _MISMATCH.  The result is wave-uniform.
 template <int MODE>
-__device__ __forceinline__ void finish_packet(const BatchParams &p, uint32_t i, uint8_t *pkt, uint32_t Ld,
-                                              uint32_t crc, bool aligned, uint32_t lane) {
-    if (lane != 0) return;
+__device__ __forceinline__ uint32_t packet_result(const BatchParams &p, uint8_t *pkt, uint32_t Ld, uint32_t crc,
+                                                  bool aligned, uint32_t lane) {
     uint8_t *tr = pkt + Ld;
     if (MODE == kCompute) {
-        if (p.out) p.out[i] = crc;
-        if (p.trailer) {
+        if (p.trailer && lane == 0) {
             if (aligned) {
                 *reinterpret_cast<uint32_t *>(tr) = crc;
             } else {
@@ -166,47 +184,67 @@ __device__ __forceinline__ void finish_packet(const BatchParams &p, uint32_t i, 
                 tr[3] = static_cast<uint8_t>(crc >> 24);
             }
         }
+        return crc;
     } else {
-        uint32_t stored;
+        uint32_t stored;  // every lane reads the same 4 bytes (one cache line)
         if (aligned) {
             stored = *reinterpret_cast<const uint32_t *>(tr);
         } else {
             stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
                      (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
         }
-        p.ok[i] = (stored == crc) ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
-        if (p.trailer) {
+        const uint32_t ok = __builtin_amdgcn_readfirstlane(stored == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH);
+        if (p.trailer && lane == 0) {  // is_icrc_valid zeroes the trailer (packet_processor.rs:350)
             if (aligned) {
                 *reinterpret_cast<uint32_t *>(tr) = 0u;
             } else {
                 tr[0] = tr[1] = tr[2] = tr[3] = 0;
             }
         }
+        return ok;
     }
 }
 
 // One packet, any length/alignment, no pipelining (variant 0, and irregular packets).
+// Returns the packet's result value (see packet_result; bad length -> 0 / ICRC_VERIFY_BADLEN).
 template <int MODE>
-__device__ __forceinline__ void handle_packet(const BatchParams &p, uint32_t i, const char *lds,
-                                           const LaneConsts &c, uint32_t lane) {
-    const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
-    const uint32_t L = p.len ? p.len[i] : p.ulen;
-    uint8_t *pkt = p.base + off;
+__device__ __forceinline__ uint32_t handle_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
+                                                  const LaneConsts &c, uint32_t lane) {
     if (L < ICRC_MIN_PACKET) {
-        if (lane == 0) {
-            if (p.nerr) atomicAdd(p.nerr, 1u);
-            if (MODE == kCompute) {
-                if (p.out) p.out[i] = 0u;
-            } else {
-                p.ok[i] = ICRC_VERIFY_BADLEN;
-            }
-        }
-        return;
+        if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
+        return MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN;
     }
     const uint32_t Ld = L - 4u;
     const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
     const uint32_t acc = fast ? fast_packet_state(lds, pkt, Ld, c, lane) : slow_packet_state(lds, pkt, Ld, c, lane);
-    finish_packet<MODE>(p, i, pkt, Ld, ~wave_xor(final_mul(lds, acc, c.fin)), fast, lane);
+    return packet_result<MODE>(p, pkt, Ld, ~wave_xor(final_mul(lds, acc, c.fin)), fast, lane);
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_result(const BatchParams &p, uint32_t i, uint32_t r) {
+    if (MODE == kCompute) {
+        if (p.out) p.out[i] = r;
+    } else {
+        p.ok[i] = static_cast<uint8_t>(r);
+    }
+}
+
+// Per-wave result buffer: result of packet q goes to lane (q & 63) of one VGPR; 64 results
+// leave as one coalesced store (256 B of ICRCs or 64 B of ok bytes).
+struct ResultBuf {
+    uint32_t v;       // per lane
+    uint64_t valid;   // uniform lane mask
+};
+
+__device__ __forceinline__ void rb_put(ResultBuf &rb, uint32_t q, uint32_t r) {
+    rb.v = (__lane_id() == (q & 63u)) ? r : rb.v;
+    rb.valid |= 1ull << (q & 63u);
+}
+
+template <int MODE>
+__device__ __forceinline__ void rb_flush(const BatchParams &p, ResultBuf &rb, uint32_t base, uint32_t lane) {
+    if ((rb.valid >> lane) & 1ull) store_result<MODE>(p, base + lane, rb.v);
+    rb.valid = 0;
 }
 
 // ---- pipelined path -----------------------------------------------------------------------
@@ -234,26 +272,25 @@ __device__ __forceinline__ bool static_for(F &&f) {
 struct SlotMeta {
     uint8_t *pkt;
     uint32_t L;
-    uint32_t idx;
     int R;      // rows (regular packets)
     int k0;     // stream index of lane 0 in row 0
     int kind;   // 0 = no packet, 1 = regular (aligned, 44 <= L, R <= kRows), 2 = irregular
 };
 
-// Ragged batches: (offset, len) of 64 consecutive packets of this wave's sequence, one per
-// lane, fetched with one vector load each and read back with v_readlane (uniform index).
+// Ragged batches: (offset, len) of 64 consecutive packets of this wave's chunk, one per lane
+// (one coalesced load each), read back with v_readlane at a wave-uniform index.
 struct MetaBlock {
     uint32_t off_lo, off_hi, len;  // per lane
     int block;                     // uniform
 };
 
-__device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, uint32_t first, uint32_t tw,
+__device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, uint32_t lo, uint32_t hi,
                                            int block, uint32_t lane) {
-    const uint64_t i = static_cast<uint64_t>(first) + (static_cast<uint64_t>(block) * 64u + lane) * tw;
+    const uint32_t i = lo + static_cast<uint32_t>(block) * 64u + lane;
     uint64_t off = 0;
     uint32_t len = 0;
-    if (i < p.n) {
-        off = p.off ? p.off[i] : i * p.stride;
+    if (i < hi) {
+        off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
         len = p.len ? p.len[i] : p.ulen;
     }
     mb.off_lo = static_cast<uint32_t>(off);
@@ -262,26 +299,25 @@ __device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, 
     mb.block = block;
 }
 
-__device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t first,
-                                          uint32_t tw, uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
+__device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t lo,
+                                          uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
     m.kind = 0;
     m.R = 0;
     m.k0 = 0;
     m.pkt = p.base;
     m.L = 0;
-    m.idx = first + q * tw;
     if (q >= nq) return;
     uint64_t off;
     uint32_t L;
     if (ragged) {
         const int block = static_cast<int>(q >> 6);
-        if (block != mb.block) meta_fetch(p, mb, first, tw, block, lane);
+        if (block != mb.block) meta_fetch(p, mb, lo, lo + nq, block, lane);
         const int l = static_cast<int>(q & 63u);
         off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
               (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
         L = __builtin_amdgcn_readlane(mb.len, l);
     } else {
-        off = static_cast<uint64_t>(m.idx) * p.stride;
+        off = static_cast<uint64_t>(lo + q) * p.stride;
         L = p.ulen;
     }
     m.pkt = p.base + off;
@@ -325,13 +361,19 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
     }
 }
 
+// Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
+// the wave's result buffer.
 template <int MODE, int S, int ABL>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows]) {
+                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows],
+                                            uint32_t q0, ResultBuf &rb) {
     int rmax = 0;
+    bool same = true;  // every slot regular with the same row count (the common case)
 #pragma unroll
-    for (int s = 0; s < S; ++s)
+    for (int s = 0; s < S; ++s) {
         if (m[s].kind == 1 && m[s].R > rmax) rmax = m[s].R;
+        same = same && m[s].kind == 1 && m[s].R == m[0].R;
+    }
     if (rmax > 0) {
         uint32_t acc[S];
 #pragma unroll
@@ -340,18 +382,31 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             acc[s] = u[s][0] | head_mask(k);
             u[s][1] |= head_mask(k + 64);
         }
-        // One straight-line block per row for all S chains (the scheduler interleaves them);
-        // a chain past its own last row keeps its value through a select.
+        // One straight-line block per row for all S chains (the scheduler interleaves them).
+        if (same) {
 #pragma unroll
-        for (int j = 1; j < kRows; ++j) {
-            if (j < rmax) {
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if constexpr (ABL == 1) {
-                        acc[s] ^= u[s][j];
-                    } else {
-                        const uint32_t t = mul_m64(lds, acc[s], c) ^ u[s][j];
-                        acc[s] = (j < m[s].R) ? t : acc[s];
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (ABL == 1) acc[s] ^= u[s][j];
+                        else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                    }
+                }
+            }
+        } else {
+            // a chain past its own last row keeps its value through a select
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (ABL == 1) {
+                            acc[s] ^= u[s][j];
+                        } else {
+                            const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
+                            acc[s] = (j < m[s].R) ? t : acc[s];
+                        }
                     }
                 }
             }
@@ -361,24 +416,32 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
 #pragma unroll
         for (int s = 0; s < S; ++s)
-            if (m[s].kind == 1) finish_packet<MODE>(p, m[s].idx, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
+            if (m[s].kind == 1)
+                rb_put(rb, q0 + s, packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane));
     }
 #pragma unroll
     for (int s = 0; s < S; ++s)
-        if (m[s].kind == 2) handle_packet<MODE>(p, m[s].idx, lds, c, lane);
+        if (m[s].kind == 2) rb_put(rb, q0 + s, handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane));
 }
 
+// A wave owns the contiguous packet range [lo, lo + nq) and walks it in sets of S packets
+// (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
+// processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
+// ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
 template <int MODE, int S, int D, int ABL>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                              uint32_t lane, uint32_t first, uint32_t tw) {
+                                              uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
-    if (first >= p.n) return;
-    const uint32_t nq = (p.n - 1u - first) / tw + 1u;  // packets of this wave
+    static_assert(64 % S == 0, "sets must not straddle a 64-packet result block");
+    if (nq == 0) return;
     const uint32_t nsets = (nq + S - 1) / S;
     const bool ragged = p.off != nullptr || p.len != nullptr;
     MetaBlock mb;
     mb.block = -1;
     mb.off_lo = mb.off_hi = mb.len = 0;
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
     SlotMeta m[B][S];
     uint32_t u[B][S][kRows];
 #pragma unroll
@@ -386,7 +449,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
         if (static_cast<uint32_t>(d) < nsets) {
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta(p, mb, ragged, first, tw, d * S + s, nq, lane, m[d][s]);
+                slot_meta(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
                 slot_load<ABL>(m[d][s], lane, u[d][s]);
             }
         }
@@ -401,11 +464,14 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             if (tp < nsets) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    slot_meta(p, mb, ragged, first, tw, tp * S + s, nq, lane, m[bp][s]);
+                    slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
                     slot_load<ABL>(m[bp][s], lane, u[bp][s]);
                 }
             }
-            process_set<MODE, S, ABL>(p, lds, c, lane, m[b], u[b]);
+            const uint32_t q0 = ts * S;
+            process_set<MODE, S, ABL>(p, lds, c, lane, m[b], u[b], q0, rb);
+            const uint32_t qn = q0 + S;  // next unprocessed
+            if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             return true;
         });
         if (!cont) return;
@@ -413,9 +479,10 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 }
 
 // Kernel variants (runtime-selected, identical results):
-//   0            one packet per wave at a time, no pipelining
-//   S, D, ABL    pipelined with S chains and a D-deep ring; ABL = 0 (real), 1 (loads only,
-//                no CRC: a memory-pipeline bound), 2 (CRC only, no loads: a compute bound).
+//   0            one packet per wave at a time, no pipelining, strided packet assignment
+//   S, D, ABL    pipelined with S chains and a D-deep ring over a contiguous packet chunk per
+//                wave; ABL = 0 (real), 1 (loads only, no CRC: a memory-pipeline bound),
+//                2 (CRC only, no loads: a compute bound).
 template <int MODE, int S, int D, int ABL>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
@@ -429,18 +496,26 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     LaneConsts c;
-    c.lo0 = (lane & 31u) * 4u;
-    c.lo1 = c.lo0 + 128u;
-    c.lo2 = c.lo0 + 65536u;
-    c.lo3 = c.lo1 + 65536u;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
 
     const uint32_t tw = gridDim.x * kWavesPerGroup;
-    const uint32_t first = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
     if constexpr (S == 0) {
-        for (uint32_t i = first; i < p.n; i += tw) handle_packet<MODE>(p, i, lds, c, lane);
+        for (uint32_t i = gw; i < p.n; i += tw) {
+            const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
+            const uint32_t L = p.len ? p.len[i] : p.ulen;
+            const uint32_t r = handle_packet<MODE>(p, p.base + off, L, lds, c, lane);
+            if (lane == 0) store_result<MODE>(p, i, r);
+        }
     } else {
-        run_pipelined<MODE, S, D, ABL>(p, lds, c, lane, first, tw);
+        // contiguous chunks, 64-packet aligned so result stores are whole blocks
+        const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+        const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+        if (lo64 >= p.n) return;
+        const uint32_t lo = static_cast<uint32_t>(lo64);
+        const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+        run_pipelined<MODE, S, D, ABL>(p, lds, c, lane, lo, nq);
     }
 }
 
@@ -511,6 +586,8 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 5: ICRC_LAUNCH(2, 2, 0); break;
     case 6: ICRC_LAUNCH(1, 2, 1); break;  // diagnostic: loads only
     case 7: ICRC_LAUNCH(1, 2, 2); break;  // diagnostic: CRC only
+    case 8: ICRC_LAUNCH(2, 1, 2); break;  // diagnostic: CRC only, 2 chains
+    case 9: ICRC_LAUNCH(2, 1, 1); break;  // diagnostic: loads only, 2 chains
     default: ICRC_LAUNCH(1, 2, 0); break;
     }
 }

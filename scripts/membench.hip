@@ -1,0 +1,144 @@
+// scripts/membench.hip — achievable HBM read bandwidth on MI355X for the ICRC access shapes
+// ("measured achievable streaming-read bandwidth ... as a secondary denominator").
+// Reads a 1 Mi x 4156-B packet batch (4.36 GB, stride 4156 = 4-byte aligned packets) in:
+//   A  flat dwordx4 grid-stride sweep (the copy-style ceiling), 16 or 32 waves/CU
+//   B  wave per packet, 256-B rows of buffer_load_dword (the v1 kernel's shape), P in flight
+//   C  wave per packet, 1-KiB rows of buffer_load_dwordx4 (16 B/lane), P in flight
+// Each kernel XOR-folds what it reads and stores one word per wave (no dead-code removal).
+// Build: hipcc --offload-arch=gfx950 -O3 -o membench membench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                 \
+        }                                                                            \
+    } while (0)
+
+constexpr uint32_t kL = 4156;
+constexpr uint32_t kN = 1u << 20;
+
+__global__ void flat_x4(const uint4 *p, size_t n16, uint32_t *out) {
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+template <int P>
+__global__ __launch_bounds__(1024) void rows_dword(const uint8_t *base, uint32_t *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    uint32_t acc = 0;
+    const int N = 1 + (kL - 4) / 4, R = (N + 63) / 64, k0 = N - 64 * R;
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave; i < kN; i += P * tw) {
+        uint32_t u[P][17];
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            uint32_t pi = i + s * tw;
+            const uint8_t *pkt = base + (size_t)(pi < kN ? pi : 0) * kL;
+            auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)pkt, 0, pi < kN ? (int)(kL - 4) : 0, 0x00020000);
+            uint32_t vb = 4u * (uint32_t)(k0 - 1 + (int)lane);
+#pragma unroll
+            for (int j = 0; j < 17; ++j) u[s][j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 256u * j), 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+#pragma unroll
+            for (int j = 0; j < 17; ++j) acc ^= u[s][j];
+    }
+    out[blockIdx.x * (blockDim.x / 64) + wave] = acc;
+}
+
+template <int P>
+__global__ __launch_bounds__(1024) void rows_x4(const uint8_t *base, uint32_t *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    uint32_t acc = 0;
+    const int N = 1 + (kL - 4) / 4, R = (N + 255) / 256, k0 = N - 256 * R;
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave; i < kN; i += P * tw) {
+        uint4 u[P][5];
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            uint32_t pi = i + s * tw;
+            const uint8_t *pkt = base + (size_t)(pi < kN ? pi : 0) * kL;
+            auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)pkt, 0, pi < kN ? (int)(kL - 4) : 0, 0x00020000);
+            uint32_t vb = 4u * (uint32_t)(k0 - 1 + 4 * (int)lane);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vb + 1024u * j), 0, 0);
+                u[s][j] = *reinterpret_cast<uint4 *>(&v);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < P; ++s)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc ^= u[s][j].x ^ u[s][j].y ^ u[s][j].z ^ u[s][j].w;
+    }
+    out[blockIdx.x * (blockDim.x / 64) + wave] = acc;
+}
+
+template <class F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    int cus = 0;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    cus = prop.multiProcessorCount;
+    const size_t bytes = (size_t)kN * kL;
+    uint8_t *d;
+    uint32_t *out;
+    CK(hipMalloc(&d, bytes + 4096));
+    CK(hipMalloc(&out, 1 << 24));
+    CK(hipMemset(d, 0x5a, bytes));
+    const int reps = 10;
+    auto report = [&](const char *name, float ms) {
+        printf("{\"pattern\": \"%s\", \"ms\": %.4f, \"GB/s\": %.1f}\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    for (int wpc : {16, 32}) {
+        int grid = cus * (wpc / 4);  // 256-thread blocks
+        float ms = time_it([&] { flat_x4<<<grid, 256>>>((const uint4 *)d, bytes / 16, out); }, reps);
+        char nm[64];
+        snprintf(nm, sizeof nm, "A flat dwordx4 %d waves/CU", wpc);
+        report(nm, ms);
+    }
+#define RUN_ROWS(K, P, NAME)                                                                     \
+    {                                                                                            \
+        float ms = time_it([&] { K<P><<<cus, 1024>>>(d, out); }, reps);                          \
+        report(NAME, ms);                                                                        \
+    }
+    RUN_ROWS(rows_dword, 1, "B dword rows, 1 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_dword, 2, "B dword rows, 2 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_dword, 3, "B dword rows, 3 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_x4, 1, "C dwordx4 rows, 1 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_x4, 2, "C dwordx4 rows, 2 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_x4, 4, "C dwordx4 rows, 4 pkt/wave in flight, 16 waves/CU")
+    CK(hipFree(d));
+    CK(hipFree(out));
+    return 0;
+}
