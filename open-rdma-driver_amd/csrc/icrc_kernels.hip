@@ -86,13 +86,17 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 
 // Fast path (4-aligned packet, L % 4 == 0): OR-masks of the stream words that carry the
 // FF prefix (k = 0) and the masked header bytes (packet.rs offsets 1, 8, 10-11, 26-27, 32).
+// Branch-free: bit j of kMaskedBytes = stream byte j is forced to 0xFF (prefix bytes 0-3,
+// packet bytes 1, 8, 10, 11, 26, 27, 32 -> stream bytes 5, 12, 14, 15, 30, 31, 36); the
+// nibble of word k is widened to byte masks (bit t -> byte t) with one multiply.
+// (Divergent compare chains here made hipcc fall back to s_waitcnt vmcnt(0), draining the
+// prefetched loads of the next packet.)
 __device__ __forceinline__ uint32_t head_mask(int k) {
-    return k == 0   ? 0xffffffffu
-           : k == 1 ? 0x0000ff00u
-           : k == 3 ? 0xffff00ffu
-           : k == 7 ? 0xffff0000u
-           : k == 9 ? 0x000000ffu
-                    : 0u;
+    const uint32_t kk = static_cast<uint32_t>(k);  // k < 0 wraps large -> 0
+    const uint32_t lo = (0xC000D02Fu >> ((kk & 7u) * 4u)) & 15u;
+    const uint32_t hi = (0x00000010u >> ((kk & 7u) * 4u)) & 15u;
+    const uint32_t nib = kk < 8u ? lo : (kk < 16u ? hi : 0u);
+    return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
 }
 
 __device__ __forceinline__ uint32_t fast_packet_state(const char *lds, const uint8_t *pkt,
@@ -334,7 +338,7 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
     }
 }
 
-// Loads in three blocks by row count (short packets issue few instructions); rows past the
+// Loads of one packet's rows; rows past the
 // packet and every row of a non-regular slot read 0 through the descriptor's range check.
 template <int ABL>
 __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[kRows]) {
@@ -346,19 +350,12 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
     const int nrec = m.kind == 1 ? static_cast<int>(m.L - 4u) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
     const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
+    // Always kRows loads, no branch: hipcc's static vmcnt accounting takes the minimum over
+    // all paths, so a conditional load block anywhere in the ring turns the waits for the
+    // current packet into vmcnt(0) and drains the prefetch of the next one.
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < kRows; ++j)
         u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
-    if (m.R > 2) {
-#pragma unroll
-        for (int j = 2; j < 8; ++j)
-            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
-    }
-    if (m.R > 8) {
-#pragma unroll
-        for (int j = 8; j < kRows; ++j)
-            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
-    }
 }
 
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
@@ -461,12 +458,11 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             const uint32_t ts = t + b;
             if (ts >= nsets) return false;
             const uint32_t tp = ts + D;
-            if (tp < nsets) {
+            // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor)
 #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
-                    slot_load<ABL>(m[bp][s], lane, u[bp][s]);
-                }
+            for (int s = 0; s < S; ++s) {
+                slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                slot_load<ABL>(m[bp][s], lane, u[bp][s]);
             }
             const uint32_t q0 = ts * S;
             process_set<MODE, S, ABL>(p, lds, c, lane, m[b], u[b], q0, rb);

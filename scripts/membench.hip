@@ -88,6 +88,48 @@ __global__ __launch_bounds__(1024) void rows_x4(const uint8_t *base, uint32_t *o
     out[blockIdx.x * (blockDim.x / 64) + wave] = acc;
 }
 
+// D: wave owns a contiguous chunk of packets (the pipelined kernel's assignment), one packet
+// prefetched ahead; STORE = 0 none, 1 per-packet 4-B store, 2 one coalesced store per 64.
+template <int STORE>
+__global__ __launch_bounds__(1024) void rows_chunk(const uint8_t *base, uint32_t *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave;
+    const uint32_t chunk = ((kN + tw - 1) / tw + 63) & ~63u;
+    const uint32_t lo = gw * chunk;
+    if (lo >= kN) return;
+    const uint32_t nq = kN - lo < chunk ? kN - lo : chunk;
+    const int N = 1 + (kL - 4) / 4, R = (N + 63) / 64, k0 = N - 64 * R;
+    const uint32_t vb = 4u * (uint32_t)(k0 - 1 + (int)lane);
+    uint32_t ua[17], ub[17], buf = 0;
+    auto load = [&](uint32_t q, uint32_t(&u)[17]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)(lo + q) * kL), 0, (int)(kL - 4), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 17; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 256u * j), 0, 0);
+    };
+    auto fold = [&](uint32_t q, uint32_t(&u)[17]) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int j = 0; j < 17; ++j) a ^= u[j];
+        a ^= __shfl_xor(a, 1);
+        if (STORE == 1 && lane == 0) out[lo + q] = a;
+        if (STORE == 2) {
+            buf = (lane == (q & 63)) ? a : buf;
+            if ((q & 63) == 63 || q + 1 == nq) out[lo + (q & ~63u) + lane] = buf;
+        }
+        if (STORE == 0 && a == 0x12345678u) out[0] = a;
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        fold(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        fold(q + 1, ub);
+    }
+}
+
 template <class F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -138,6 +180,10 @@ int main() {
     RUN_ROWS(rows_x4, 1, "C dwordx4 rows, 1 pkt/wave in flight, 16 waves/CU")
     RUN_ROWS(rows_x4, 2, "C dwordx4 rows, 2 pkt/wave in flight, 16 waves/CU")
     RUN_ROWS(rows_x4, 4, "C dwordx4 rows, 4 pkt/wave in flight, 16 waves/CU")
+    RUN_ROWS(rows_chunk, 0, "D chunked dword rows, prefetch 1, no stores")
+    RUN_ROWS(rows_chunk, 1, "D chunked dword rows, prefetch 1, per-packet 4-B store")
+    RUN_ROWS(rows_chunk, 2, "D chunked dword rows, prefetch 1, coalesced store per 64")
+    RUN_ROWS(rows_dword, 1, "B dword rows, 1 pkt/wave in flight, 16 waves/CU (again)")
     CK(hipFree(d));
     CK(hipFree(out));
     return 0;
