@@ -12,22 +12,38 @@
 
 #include "icrc_internal.h"
 
+namespace {
+
+// One stage of the host-resident pipeline: device + pinned host buffers, a stream, an event.
+struct Stage {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t *d_buf = nullptr;
+    size_t d_cap = 0;
+    uint64_t *d_off = nullptr;
+    uint32_t *d_len = nullptr;
+    uint32_t *d_res = nullptr;
+    size_t meta_cap = 0;
+    uint8_t *h_buf = nullptr;  // pinned gather buffer
+    size_t h_cap = 0;
+    uint64_t *h_off = nullptr;  // pinned
+    uint32_t *h_len = nullptr;  // pinned
+    uint32_t *h_res = nullptr;  // pinned
+    // chunk in flight
+    bool busy = false;
+    uint32_t i0 = 0, cnt = 0;
+};
+
+}  // namespace
+
 struct icrc_engine {
     int device = 0;
     int num_cu = 0;
     int variant = icrc::kDefaultVariant;
     uint32_t *d_table = nullptr;
     hipStream_t stream = nullptr;
-    std::mutex mu;  // guards the staging buffers below
-    // host-batch / scalar staging
-    uint8_t *d_stage = nullptr;
-    size_t d_stage_cap = 0;
-    uint64_t *d_off = nullptr;
-    uint32_t *d_len = nullptr;
-    uint32_t *d_res = nullptr;  // ICRCs or ok bytes
-    size_t d_meta_cap = 0;      // packets
-    uint8_t *h_stage = nullptr; // pinned
-    size_t h_stage_cap = 0;
+    std::mutex mu;  // guards the host-batch stages
+    Stage st[2];
 };
 
 namespace {
@@ -57,55 +73,124 @@ int grid_for(const icrc_engine *e, uint32_t n) {
     return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(want, static_cast<uint64_t>(e->num_cu))));
 }
 
-int ensure_device_stage(icrc_engine *e, size_t bytes, size_t pkts) {
-    if (bytes > e->d_stage_cap) {
-        if (e->d_stage) (void)hipFree(e->d_stage);
-        e->d_stage = nullptr;
-        e->d_stage_cap = 0;
-        size_t cap = std::max<size_t>(bytes, 1 << 20);
-        if (hipMalloc(&e->d_stage, cap + 64) != hipSuccess) return ICRC_ENOMEM;
-        e->d_stage_cap = cap;
+void stage_free(Stage &s) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_len) (void)hipFree(s.d_len);
+    if (s.d_res) (void)hipFree(s.d_res);
+    if (s.h_buf) (void)hipHostFree(s.h_buf);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_len) (void)hipHostFree(s.h_len);
+    if (s.h_res) (void)hipHostFree(s.h_res);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Stage{};
+}
+
+int stage_reserve(Stage &s, size_t bytes, size_t pkts, bool need_host_buf) {
+    if (!s.stream) {
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return ICRC_EDEVICE;
+        if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return ICRC_EDEVICE;
     }
-    if (pkts > e->d_meta_cap) {
-        if (e->d_off) (void)hipFree(e->d_off);
-        if (e->d_len) (void)hipFree(e->d_len);
-        if (e->d_res) (void)hipFree(e->d_res);
-        e->d_off = nullptr;
-        e->d_len = nullptr;
-        e->d_res = nullptr;
-        e->d_meta_cap = 0;
-        size_t cap = std::max<size_t>(pkts, 4096);
-        if (hipMalloc(&e->d_off, cap * sizeof(uint64_t)) != hipSuccess) return ICRC_ENOMEM;
-        if (hipMalloc(&e->d_len, cap * sizeof(uint32_t)) != hipSuccess) return ICRC_ENOMEM;
-        if (hipMalloc(&e->d_res, cap * sizeof(uint32_t)) != hipSuccess) return ICRC_ENOMEM;
-        e->d_meta_cap = cap;
+    if (bytes > s.d_cap) {
+        if (s.d_buf) (void)hipFree(s.d_buf);
+        s.d_buf = nullptr;
+        s.d_cap = 0;
+        const size_t cap = std::max<size_t>(bytes, size_t(1) << 20);
+        if (hipMalloc(&s.d_buf, cap + 64) != hipSuccess) return ICRC_ENOMEM;
+        s.d_cap = cap;
+    }
+    if (need_host_buf && bytes > s.h_cap) {
+        if (s.h_buf) (void)hipHostFree(s.h_buf);
+        s.h_buf = nullptr;
+        s.h_cap = 0;
+        const size_t cap = std::max<size_t>(bytes, size_t(1) << 20);
+        if (hipHostMalloc(&s.h_buf, cap, hipHostMallocDefault) != hipSuccess) return ICRC_ENOMEM;
+        s.h_cap = cap;
+    }
+    if (pkts > s.meta_cap) {
+        for (void *p : {static_cast<void *>(s.d_off), static_cast<void *>(s.d_len), static_cast<void *>(s.d_res)})
+            if (p) (void)hipFree(p);
+        for (void *p : {static_cast<void *>(s.h_off), static_cast<void *>(s.h_len), static_cast<void *>(s.h_res)})
+            if (p) (void)hipHostFree(p);
+        s.d_off = nullptr;
+        s.d_len = nullptr;
+        s.d_res = nullptr;
+        s.h_off = nullptr;
+        s.h_len = nullptr;
+        s.h_res = nullptr;
+        s.meta_cap = 0;
+        const size_t cap = std::max<size_t>(pkts, 4096);
+        if (hipMalloc(&s.d_off, cap * 8) != hipSuccess || hipMalloc(&s.d_len, cap * 4) != hipSuccess ||
+            hipMalloc(&s.d_res, cap * 4) != hipSuccess ||
+            hipHostMalloc(&s.h_off, cap * 8, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&s.h_len, cap * 4, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&s.h_res, cap * 4, hipHostMallocDefault) != hipSuccess)
+            return ICRC_ENOMEM;
+        s.meta_cap = cap;
     }
     return ICRC_OK;
 }
 
-int ensure_host_stage(icrc_engine *e, size_t bytes) {
-    if (bytes <= e->h_stage_cap) return ICRC_OK;
-    if (e->h_stage) (void)hipHostFree(e->h_stage);
-    e->h_stage = nullptr;
-    e->h_stage_cap = 0;
-    size_t cap = std::max<size_t>(bytes, 1 << 20);
-    if (hipHostMalloc(&e->h_stage, cap, hipHostMallocDefault) != hipSuccess) return ICRC_ENOMEM;
-    e->h_stage_cap = cap;
-    return ICRC_OK;
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error; clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
 }
 
 std::mutex g_registry_mu;
 std::map<int, icrc_engine *> g_default;
-
-// Host-resident batch: stage packets [lo, hi) of one chunk into device memory, run the
-// kernel, return ICRCs (mode compute) or ok bytes (mode verify) in e->d_res.
-constexpr size_t kChunkBytes = size_t(256) << 20;
 
 int validate_host(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n) {
     if (n == 0) return ICRC_OK;
     if (!base || !off || !len) return ICRC_EINVAL;
     for (uint32_t i = 0; i < n; i++)
         if (len[i] < ICRC_MIN_PACKET) return ICRC_EINVAL;  // the reference panics here
+    return ICRC_OK;
+}
+
+// Host-resident batch, pipelined over two stages: chunk c+1 is copied H2D while chunk c's
+// kernel runs.  Pinned, compact batches are copied as one span per chunk (no CPU copy);
+// otherwise packets are gathered into pinned staging first.  Trailers (write / zero) are
+// applied to the caller's host buffer from the returned results.
+constexpr size_t kChunkBytes = size_t(64) << 20;
+
+struct HostJob {
+    int mode;
+    uint8_t *base;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint32_t *out;
+    uint8_t *ok;
+    int trailer;
+};
+
+int finish_stage(icrc_engine *e, Stage &s, const HostJob &j) {
+    if (!s.busy) return ICRC_OK;
+    s.busy = false;
+    HIP_TRY(hipEventSynchronize(s.done));
+    for (uint32_t i = 0; i < s.cnt; i++) {
+        const uint32_t k = s.i0 + i;
+        uint8_t *t = j.base + j.off[k] + j.len[k] - 4;
+        if (j.mode == icrc::kCompute) {
+            const uint32_t c = s.h_res[i];
+            if (j.out) j.out[k] = c;
+            if (j.trailer) {
+                t[0] = uint8_t(c);
+                t[1] = uint8_t(c >> 8);
+                t[2] = uint8_t(c >> 16);
+                t[3] = uint8_t(c >> 24);
+            }
+        } else {
+            j.ok[k] = reinterpret_cast<const uint8_t *>(s.h_res)[i];
+            if (j.trailer) std::memset(t, 0, 4);
+        }
+    }
+    (void)e;
     return ICRC_OK;
 }
 
@@ -120,69 +205,78 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
     DeviceGuard g(e->device);
     if (!g.ok) return ICRC_ENODEV;
     std::lock_guard<std::mutex> lk(e->mu);
-    std::vector<uint64_t> doff;
-    std::vector<uint32_t> res;
+    const HostJob job{mode, base, off, len, out_icrc, ok, trailer};
+    const bool pinned = host_pinned(base);
+    int rc = ICRC_OK;
     uint32_t i0 = 0;
-    while (i0 < n) {
-        // Grow the chunk while the packed size stays under kChunkBytes.
+    for (int c = 0; i0 < n && rc == ICRC_OK; ++c) {
+        Stage &s = e->st[c & 1];
+        if ((rc = finish_stage(e, s, job)) != ICRC_OK) break;
+        // chunk [i0, i1): packed size <= kChunkBytes (at least one packet)
         uint32_t i1 = i0;
         size_t packed = 0;
-        while (i1 < n && (i1 == i0 || packed + len[i1] <= kChunkBytes)) {
+        uint64_t smin = UINT64_MAX, smax = 0;
+        while (i1 < n && (i1 == i0 || packed + len[i1] + 3 <= kChunkBytes)) {
             packed += (static_cast<size_t>(len[i1]) + 3) & ~size_t(3);
+            smin = std::min<uint64_t>(smin, off[i1]);
+            smax = std::max<uint64_t>(smax, off[i1] + len[i1]);
             i1++;
         }
         const uint32_t cnt = i1 - i0;
-        int rc = ensure_device_stage(e, packed, cnt);
-        if (rc) return rc;
-        rc = ensure_host_stage(e, packed);
-        if (rc) return rc;
-        // Gather into pinned staging (4-aligned slots so the kernel takes its fast path).
-        doff.resize(cnt);
-        size_t pos = 0;
-        for (uint32_t i = 0; i < cnt; i++) {
-            std::memcpy(e->h_stage + pos, base + off[i0 + i], len[i0 + i]);
-            doff[i] = pos;
-            pos += (static_cast<size_t>(len[i0 + i]) + 3) & ~size_t(3);
-        }
-        HIP_TRY(hipMemcpyAsync(e->d_stage, e->h_stage, pos, hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(hipMemcpyAsync(e->d_off, doff.data(), cnt * sizeof(uint64_t), hipMemcpyHostToDevice, e->stream));
-        HIP_TRY(hipMemcpyAsync(e->d_len, len + i0, cnt * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
-        BatchParams p{};
-        p.base = e->d_stage;
-        p.off = e->d_off;
-        p.len = e->d_len;
-        p.n = cnt;
-        p.table = e->d_table;
-        p.trailer = 0;  // trailers are written on the host copy below
-        p.variant = e->variant;
-        if (mode == icrc::kCompute) p.out = e->d_res;
-        else p.ok = reinterpret_cast<uint8_t *>(e->d_res);
-        rc = icrc::launch_batch(mode, p, grid_for(e, cnt), e->stream);
-        if (rc) return rc;
-        if (mode == icrc::kCompute) {
-            res.resize(cnt);
-            HIP_TRY(hipMemcpyAsync(res.data(), e->d_res, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-            HIP_TRY(hipStreamSynchronize(e->stream));
-            for (uint32_t i = 0; i < cnt; i++) {
-                if (out_icrc) out_icrc[i0 + i] = res[i];
-                if (trailer) {
-                    uint8_t *t = base + off[i0 + i] + len[i0 + i] - 4;
-                    const uint32_t c = res[i];
-                    t[0] = uint8_t(c);
-                    t[1] = uint8_t(c >> 8);
-                    t[2] = uint8_t(c >> 16);
-                    t[3] = uint8_t(c >> 24);
-                }
+        const bool direct = pinned && (smax - smin) <= packed + packed / 4 + 4096;
+        const size_t dev_bytes = direct ? static_cast<size_t>(smax - smin) : packed;
+        if ((rc = stage_reserve(s, dev_bytes, cnt, !direct)) != ICRC_OK) break;
+        std::memcpy(s.h_len, len + i0, cnt * sizeof(uint32_t));
+        if (direct) {
+            for (uint32_t i = 0; i < cnt; i++) s.h_off[i] = off[i0 + i] - smin;
+            if (hipMemcpyAsync(s.d_buf, base + smin, dev_bytes, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+                rc = ICRC_EDEVICE;
+                break;
             }
         } else {
-            HIP_TRY(hipMemcpyAsync(ok + i0, e->d_res, cnt, hipMemcpyDeviceToHost, e->stream));
-            HIP_TRY(hipStreamSynchronize(e->stream));
-            if (trailer)
-                for (uint32_t i = 0; i < cnt; i++) std::memset(base + off[i0 + i] + len[i0 + i] - 4, 0, 4);
+            size_t pos = 0;
+            for (uint32_t i = 0; i < cnt; i++) {
+                std::memcpy(s.h_buf + pos, base + off[i0 + i], len[i0 + i]);
+                s.h_off[i] = pos;
+                pos += (static_cast<size_t>(len[i0 + i]) + 3) & ~size_t(3);
+            }
+            if (hipMemcpyAsync(s.d_buf, s.h_buf, pos, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+                rc = ICRC_EDEVICE;
+                break;
+            }
         }
+        if (hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+            hipMemcpyAsync(s.d_len, s.h_len, cnt * 4, hipMemcpyHostToDevice, s.stream) != hipSuccess) {
+            rc = ICRC_EDEVICE;
+            break;
+        }
+        BatchParams p{};
+        p.base = s.d_buf;
+        p.off = s.d_off;
+        p.len = s.d_len;
+        p.n = cnt;
+        p.table = e->d_table;
+        p.trailer = 0;  // trailers are applied to the caller's host copy in finish_stage
+        p.variant = e->variant;
+        if (mode == icrc::kCompute) p.out = s.d_res;
+        else p.ok = reinterpret_cast<uint8_t *>(s.d_res);
+        if ((rc = icrc::launch_batch(mode, p, grid_for(e, cnt), s.stream)) != ICRC_OK) break;
+        const size_t res_bytes = mode == icrc::kCompute ? cnt * 4 : cnt;
+        if (hipMemcpyAsync(s.h_res, s.d_res, res_bytes, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+            hipEventRecord(s.done, s.stream) != hipSuccess) {
+            rc = ICRC_EDEVICE;
+            break;
+        }
+        s.busy = true;
+        s.i0 = i0;
+        s.cnt = cnt;
         i0 = i1;
     }
-    return ICRC_OK;
+    for (Stage &s : e->st) {
+        const int r2 = finish_stage(e, s, job);
+        if (rc == ICRC_OK) rc = r2;
+    }
+    return rc;
 }
 
 int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
@@ -215,8 +309,8 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
 extern "C" {
 
 const char *icrc_version(void) {
-    return "icrc_amd 0.1 gfx950: wave-per-packet end-aligned column Horner, LDS M^64 byte tables "
-           "(32x bank-replicated) + per-lane M^(64-l) nibble tables";
+    return "icrc_amd 0.2 gfx950: wave-per-packet end-aligned column Horner, LDS M^64 byte tables "
+           "(32x bank-replicated) + per-lane M^(64-l) nibble tables, prefetch ring, coalesced results";
 }
 
 int icrc_device_count(void) {
@@ -262,12 +356,8 @@ int icrc_engine_destroy(icrc_engine *e) {
     {
         DeviceGuard g(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
+        for (Stage &s : e->st) stage_free(s);
         if (e->d_table) (void)hipFree(e->d_table);
-        if (e->d_stage) (void)hipFree(e->d_stage);
-        if (e->d_off) (void)hipFree(e->d_off);
-        if (e->d_len) (void)hipFree(e->d_len);
-        if (e->d_res) (void)hipFree(e->d_res);
-        if (e->h_stage) (void)hipHostFree(e->h_stage);
         if (e->stream) (void)hipStreamDestroy(e->stream);
     }
     {

@@ -39,7 +39,7 @@ struct BatchParams {
 };
 
 constexpr int kDefaultVariant = 1;
-constexpr int kMaxVariant = 9;
+constexpr int kMaxVariant = 12;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

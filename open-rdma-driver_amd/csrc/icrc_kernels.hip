@@ -474,6 +474,199 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     }
 }
 
+// ---- row-stream path ------------------------------------------------------------------------
+// A wave's chunk is one flat sequence of 256-byte rows (the sum of R over its regular packets,
+// in packet order).  A ring of RD row loads stays in flight (RD * 256 B per wave); the
+// process side consumes rows in the same order, restarting the Horner accumulator at each
+// packet's first row and finalising at its last.  A short packet costs only its own rows,
+// a long one needs no special path, and every ring load is unconditional (exact vmcnt
+// accounting).  Misaligned packets and L % 4 != 0 are skipped by the stream and done by a
+// tail loop; L < 44 packets are recorded as errors when the process cursor passes them.
+struct RowCursor {  // wave-uniform
+    uint32_t q;     // packet sequence number within the chunk
+    int j;          // row within the packet
+    int R;          // rows of the current packet (0 = past the end)
+    int k0;
+    uint8_t *pkt;
+    uint32_t L;
+};
+
+// R >= 1: regular packet; 0: L < 44 (error); -1: irregular (generic path).
+__device__ __forceinline__ int classify(const uint8_t *pkt, uint32_t L, int &k0) {
+    if (L < ICRC_MIN_PACKET) return 0;
+    if (((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) != 0) return -1;
+    const int N = 1 + static_cast<int>((L - 4u) >> 2);
+    const int R = (N + 63) >> 6;
+    k0 = N - 64 * R;
+    return R;
+}
+
+__device__ __forceinline__ void meta_read(const MetaBlock &mb, uint32_t q, uint64_t &off, uint32_t &L) {
+    const int l = static_cast<int>(q & 63u);
+    off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
+          (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
+    L = __builtin_amdgcn_readlane(mb.len, l);
+}
+
+// Result buffer keyed by 64-packet block: switching block flushes the previous one.
+template <int MODE>
+__device__ __forceinline__ void rb_record(const BatchParams &p, ResultBuf &rb, int &rb_block, uint32_t lo,
+                                          uint32_t q, uint32_t r, uint32_t lane) {
+    const int blk = static_cast<int>(q >> 6);
+    if (blk != rb_block) {
+        if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+        rb_block = blk;
+    }
+    rb_put(rb, q, r);
+}
+
+template <int MODE, int RD>
+__device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                              uint32_t lane, uint32_t lo, uint32_t nq) {
+    if (nq == 0) return;
+    const bool ragged = p.off != nullptr || p.len != nullptr;
+    MetaBlock ml, mprev;  // load-side block and the one before it (the process side lags)
+    ml.block = mprev.block = -1;
+    ml.off_lo = ml.off_hi = ml.len = 0;
+    mprev.off_lo = mprev.off_hi = mprev.len = 0;
+    bool irregular = false;
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    int rb_block = -1;
+
+    auto meta_at = [&](uint32_t q, bool load_side, uint64_t &off, uint32_t &L) __attribute__((always_inline)) {
+        if (!ragged) {
+            off = static_cast<uint64_t>(lo + q) * p.stride;
+            L = p.ulen;
+            return;
+        }
+        const int blk = static_cast<int>(q >> 6);
+        if (load_side) {
+            if (blk != ml.block) {
+                mprev = ml;
+                meta_fetch(p, ml, lo, lo + nq, blk, lane);
+            }
+            meta_read(ml, q, off, L);
+        } else if (blk == ml.block) {
+            meta_read(ml, q, off, L);
+        } else if (blk == mprev.block) {
+            meta_read(mprev, q, off, L);
+        } else {  // only after a long run of skipped packets
+            MetaBlock t;
+            meta_fetch(p, t, lo, lo + nq, blk, lane);
+            meta_read(t, q, off, L);
+        }
+    };
+
+    // Advance a cursor to the next packet that has rows.  The process side also records
+    // L < 44 packets as errors and notes irregular ones for the tail loop.
+    auto next_packet = [&](RowCursor &cur, bool load_side) __attribute__((always_inline)) {
+        for (;;) {
+            cur.q += 1u;
+            if (cur.q >= nq) {
+                cur.R = 0;
+                cur.pkt = p.base;
+                cur.L = 0;
+                cur.k0 = 0;
+                cur.j = 0;
+                return;
+            }
+            uint64_t off;
+            uint32_t L;
+            meta_at(cur.q, load_side, off, L);
+            uint8_t *pkt = p.base + off;
+            int k0 = 0;
+            const int R = classify(pkt, L, k0);
+            if (R > 0) {
+                cur.R = R;
+                cur.k0 = k0;
+                cur.pkt = pkt;
+                cur.L = L;
+                cur.j = 0;
+                return;
+            }
+            if (!load_side) {
+                if (R < 0) {
+                    irregular = true;
+                } else {
+                    if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
+                    rb_record<MODE>(p, rb, rb_block, lo, cur.q, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN, lane);
+                }
+            }
+        }
+    };
+
+    RowCursor lc, pc;
+    lc.q = pc.q = 0xFFFFFFFFu;
+    next_packet(lc, true);
+    next_packet(pc, false);
+
+    // one row load per ring slot; past the end the descriptor has zero size (load -> 0)
+    auto load_row = [&](uint32_t &dst) __attribute__((always_inline)) {
+        const int nrec = lc.R > 0 ? static_cast<int>(lc.L - 4u) : 0;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(lc.pkt, 0, nrec, 0x00020000);
+        const uint32_t voff = 4u * static_cast<uint32_t>(lc.k0 - 1 + static_cast<int>(lane)) + 256u * static_cast<uint32_t>(lc.j);
+        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, 0);
+        if (lc.R > 0) {
+            lc.j += 1;
+            if (lc.j == lc.R) next_packet(lc, true);
+        }
+    };
+
+    uint32_t ring[RD];
+    static_for<RD>([&](auto ic) __attribute__((always_inline)) -> bool {
+        load_row(ring[decltype(ic)::value]);
+        return true;
+    });
+
+    uint32_t acc = 0;
+    while (pc.R > 0) {
+        static_for<RD>([&](auto ic) __attribute__((always_inline)) -> bool {
+            constexpr int i = decltype(ic)::value;
+            if (pc.R == 0) return false;
+            uint32_t u = ring[i];
+            if (pc.j < 2) u |= head_mask(pc.k0 + static_cast<int>(lane) + 64 * pc.j);
+            if (pc.j == 0) acc = u;
+            else acc = step_m64(lds, acc, u, c);
+            pc.j += 1;
+            if (pc.j == pc.R) {
+                const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
+                const uint32_t r = packet_result<MODE>(p, pc.pkt, pc.L - 4u, crc, true, lane);
+                rb_record<MODE>(p, rb, rb_block, lo, pc.q, r, lane);
+                next_packet(pc, false);
+            }
+            load_row(ring[i]);
+            return true;
+        });
+    }
+    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+
+    if (irregular) {  // misaligned packets / L % 4 != 0: the generic per-packet path
+        MetaBlock t;
+        t.block = -1;
+        t.off_lo = t.off_hi = t.len = 0;
+        for (uint32_t q = 0; q < nq; ++q) {
+            uint64_t off;
+            uint32_t L;
+            if (!ragged) {
+                off = static_cast<uint64_t>(lo + q) * p.stride;
+                L = p.ulen;
+            } else {
+                const int blk = static_cast<int>(q >> 6);
+                if (blk != t.block) meta_fetch(p, t, lo, lo + nq, blk, lane);
+                meta_read(t, q, off, L);
+            }
+            uint8_t *pkt = p.base + off;
+            int k0 = 0;
+            if (classify(pkt, L, k0) < 0) {
+                const uint32_t r = handle_packet<MODE>(p, pkt, L, lds, c, lane);
+                if (lane == 0) store_result<MODE>(p, lo + q, r);
+            }
+        }
+    }
+}
+
 // Kernel variants (runtime-selected, identical results):
 //   0            one packet per wave at a time, no pipelining, strided packet assignment
 //   S, D, ABL    pipelined with S chains and a D-deep ring over a contiguous packet chunk per
@@ -497,7 +690,14 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
-    if constexpr (S == 0) {
+    if constexpr (S < 0) {
+        const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+        const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+        if (lo64 >= p.n) return;
+        const uint32_t lo = static_cast<uint32_t>(lo64);
+        const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+        run_rowstream<MODE, -S>(p, lds, c, lane, lo, nq);
+    } else if constexpr (S == 0) {
         for (uint32_t i = gw; i < p.n; i += tw) {
             const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
             const uint32_t L = p.len ? p.len[i] : p.ulen;
@@ -584,6 +784,9 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 7: ICRC_LAUNCH(1, 2, 2); break;  // diagnostic: CRC only
     case 8: ICRC_LAUNCH(2, 1, 2); break;  // diagnostic: CRC only, 2 chains
     case 9: ICRC_LAUNCH(2, 1, 1); break;  // diagnostic: loads only, 2 chains
+    case 10: ICRC_LAUNCH(-16, 0, 0); break;  // row stream, 16 rows in flight per wave
+    case 11: ICRC_LAUNCH(-24, 0, 0); break;  // row stream, 24 rows
+    case 12: ICRC_LAUNCH(-32, 0, 0); break;  // row stream, 32 rows
     default: ICRC_LAUNCH(1, 2, 0); break;
     }
 }

@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
@@ -236,6 +236,25 @@ def test_host_batch_and_scalar_surface():
     for L in (44, 45, 46, 47, 1000, 1001):
         p = rng.integers(0, 256, L, dtype=np.uint8)
         assert icrc_amd.compute_icrc(p) == oracle.compute_icrc(p)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batch_multi_chunk(engine, pinned):
+    """Host-resident path over several 64 MiB chunks (two pipelined stages), pinned (direct
+    span copies) and pageable (gathered), with write_trailer applied to the host buffer."""
+    n = 20000
+    buf, off, lens = oracle.synth_middle_stream(n)
+    want = oracle_icrcs(buf, off, lens)
+    if pinned:
+        t = torch.empty(buf.size, dtype=torch.uint8, pin_memory=True)
+        host = t.numpy()
+        host[:] = buf
+    else:
+        host = buf.copy()
+    host[np.asarray(off + lens.astype(np.uint64) - 4, np.int64)[:, None] + np.arange(4)] = 0
+    got = engine.compute_batch_host(host, off, lens, write_trailer=True)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(host, buf)  # trailers written back == the oracle's packets
 
 
 def test_packet_writer_matches_oracle():
