@@ -134,6 +134,53 @@ typedef struct icrc_synth_desc {
 int icrc_synth_device(icrc_engine *engine, uint8_t *d_base, const icrc_synth_desc *d_desc,
                       const uint8_t *d_hdr, uint32_t n, void *stream);
 
+/* ---- fused send packetizer (§8f rows 1 + 3) -------------------------------------------------
+ * The emulator's whole send step for RDMA WRITE / READ RESPONSE messages, on the device, in one
+ * kernel: MTU segmentation (generate_segments_from_request, queues/send/operations/
+ * common.rs:152-176), per-packet opcode / PSN / ack_req / RETH (write.rs:31-96,
+ * read_response.rs:30-95, send_write_message common.rs:73-132), header serialisation and
+ * payload copy (PacketWriter::write, packet_processor.rs:210-265), zero pad, and the ICRC
+ * (computed from the words in registers, no re-read) written as the trailer.
+ *
+ * Packet s of message m is written at d_wire + m.out_offset + s * m.slot_stride; its length
+ * goes to d_pkt_len[m.first_packet + s] and its ICRC to d_icrc[m.first_packet + s] (both may
+ * be NULL).  Payload bytes come from d_src[m.payload_offset + segment start ...].  The
+ * fast path needs (payload_offset - local_va) % 4 == 0 and out_offset, slot_stride % 4 == 0;
+ * other messages take a byte-wise path with identical results. */
+typedef struct icrc_write_msg {
+    uint64_t local_va;       /* source VA of the payload: drives the first segment length */
+    uint64_t remote_va;      /* RETH va of the first packet */
+    uint64_t payload_offset; /* byte offset of the message payload in d_src */
+    uint64_t out_offset;     /* byte offset of packet 0 in d_wire */
+    uint32_t total_len;      /* sge.len: bytes to send, drives segmentation */
+    uint32_t reth_len;       /* common.total_len: the RETH len of every packet (common.rs:113) */
+    uint32_t pmtu;           /* 256 .. 4096 */
+    uint32_t rkey;
+    uint32_t dqpn;
+    uint32_t psn;            /* PSN of packet 0 (wraps at 24 bits) */
+    uint32_t src_ip, dst_ip; /* host order; the emulator uses 192.168.0.2 (common.rs:124) */
+    uint32_t first_packet;   /* index of packet 0 in the flattened packet arrays */
+    uint32_t npackets;       /* icrc_write_segment_count(local_va, total_len, pmtu) */
+    uint32_t slot_stride;    /* bytes between consecutive packets of this message */
+    uint16_t msn;            /* carried in the BTH pkey field (common.rs:91-92) */
+    uint16_t ip_id;          /* generate_payload_from_msg uses 1 (net/util.rs:179) */
+    uint8_t kind;            /* 0 = RDMA WRITE, 1 = RDMA READ RESPONSE */
+    uint8_t tran_type;       /* RC = 0 */
+    uint8_t _pad[6];
+} icrc_write_msg; /* 88 bytes */
+/* Number of packets generate_segments_from_request yields (common.rs:152-176); 0 if pmtu == 0. */
+uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu);
+/* Wire length of segment s (IPv4 + UDP + BTH + RETH + payload + pad + ICRC). */
+uint32_t icrc_write_packet_len(uint64_t local_va, uint32_t total_len, uint32_t pmtu, uint32_t s);
+/* d_msgs is device memory, sorted by first_packet, first_packet[0] == 0, packets contiguous
+ * (first_packet[m+1] == first_packet[m] + npackets[m]), sum of npackets == npackets.  A packet
+ * whose slot would run past wire_bytes (or whose payload lies outside d_src) is not written:
+ * its d_pkt_len entry is 0. */
+int icrc_write_packetize_device(icrc_engine *engine, const uint8_t *d_src, uint64_t src_bytes,
+                                const icrc_write_msg *d_msgs, uint32_t nmsgs, uint32_t npackets,
+                                uint8_t *d_wire, uint64_t wire_bytes, uint32_t *d_pkt_len,
+                                uint32_t *d_icrc, void *stream);
+
 /* ---- packet writer (PacketWriter, packet_processor.rs:150-265) -------------------------- */
 /* Flattened RdmaMessage (third_party/net/types.rs; Metadata::General / ::Acknowledge). */
 typedef struct icrc_rdma_msg {

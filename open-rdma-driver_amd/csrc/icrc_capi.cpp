@@ -497,6 +497,48 @@ int icrc_synth_device(icrc_engine *e, uint8_t *d_base, const icrc_synth_desc *d_
     return icrc::launch_synth(d_base, d_desc, d_hdr, n, stream);
 }
 
+uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {
+    if (pmtu == 0) return 0;
+    const uint32_t first = icrc::write_first_segment(local_va, total_len, pmtu);
+    const uint32_t rest = total_len - first;
+    return 1u + rest / pmtu + (rest % pmtu ? 1u : 0u);
+}
+
+uint32_t icrc_write_packet_len(uint64_t local_va, uint32_t total_len, uint32_t pmtu, uint32_t s) {
+    const uint32_t n = icrc_write_segment_count(local_va, total_len, pmtu);
+    if (s >= n) return 0;
+    const uint32_t first = icrc::write_first_segment(local_va, total_len, pmtu);
+    uint32_t len = first;
+    if (s > 0) {
+        const uint32_t start = first + (s - 1) * pmtu;
+        len = std::min(pmtu, total_len - start);
+    }
+    return 56u + len + ((4u - (len & 3u)) & 3u) + 4u;
+}
+
+int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t src_bytes,
+                                const icrc_write_msg *d_msgs, uint32_t nmsgs, uint32_t npackets,
+                                uint8_t *d_wire, uint64_t wire_bytes, uint32_t *d_pkt_len, uint32_t *d_icrc,
+                                void *stream) {
+    if (npackets == 0) return ICRC_OK;
+    if (!e || !d_msgs || nmsgs == 0 || !d_wire || (!d_src && src_bytes != 0)) return ICRC_EINVAL;
+    if (reinterpret_cast<uintptr_t>(d_msgs) % alignof(icrc_write_msg) != 0) return ICRC_EINVAL;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    icrc::PacketizeParams p;
+    p.src = d_src;
+    p.src_bytes = d_src ? src_bytes : 0;
+    p.msgs = d_msgs;
+    p.nmsgs = nmsgs;
+    p.npackets = npackets;
+    p.wire = d_wire;
+    p.wire_bytes = wire_bytes;
+    p.pkt_len = d_pkt_len;
+    p.icrc = d_icrc;
+    p.table = e->d_table;
+    return icrc::launch_packetize(p, grid_for(e, npackets), stream);
+}
+
 // Host-only helper for tests: the LDS table image (no GPU needed).
 int icrc_table_image(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;

@@ -50,5 +50,24 @@ constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
+struct PacketizeParams {
+    const uint8_t *src;
+    uint64_t src_bytes;
+    const icrc_write_msg *msgs;
+    uint32_t nmsgs;
+    uint32_t npackets;
+    uint8_t *wire;
+    uint64_t wire_bytes;
+    uint32_t *pkt_len;
+    uint32_t *icrc;
+    const uint32_t *table;
+};
+int launch_packetize(const PacketizeParams &p, int grid, void *stream);
+
+// Segmentation shared by host and tests (generate_segments_from_request, common.rs:152-176).
+inline uint32_t write_first_segment(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {
+    const uint32_t first = pmtu - static_cast<uint32_t>(local_va) % pmtu;
+    return total_len < first ? total_len : first;
+}
 
 }  // namespace icrc

@@ -715,6 +715,347 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     }
 }
 
+// ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
+// One wavefront per packet, the same row-stream ring as above, but a "row" is built rather
+// than read: header words come from the message descriptor (computed on the scalar unit,
+// placed per lane by selects), payload words from the memory-region buffer (one coalesced
+// buffer_load_dword per lane per row).  Each word is stored to the wire buffer and folded into
+// the ICRC in the same step; the ICRC is the trailer.  Byte-identical to PacketWriter::write.
+
+struct PacketHdr {  // wave-uniform; words are the LE u32 of header bytes 4w .. 4w+3
+    uint32_t w[14];
+};
+
+// Segment s of a message (generate_segments_from_request + Write::handle / ReadResponse::handle)
+struct SegInfo {
+    uint32_t start, len, L, pad;
+    uint64_t out;       // packet offset in d_wire
+    uint64_t src;       // payload offset in d_src
+    int R, k0;
+};
+
+struct MsgRegs {  // the 88-byte icrc_write_msg, one dword per lane (lanes 0..21)
+    uint32_t v;
+    int idx;  // uniform: message index held, -1 = none
+};
+
+__device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return __builtin_amdgcn_readlane(m.v, dw); }
+__device__ __forceinline__ uint64_t msg_u64(const MsgRegs &m, int dw) {
+    return static_cast<uint64_t>(msg_u32(m, dw)) | (static_cast<uint64_t>(msg_u32(m, dw + 1)) << 32);
+}
+// icrc_write_msg dword offsets
+enum : int {
+    kMLocalVa = 0, kMRemoteVa = 2, kMPayloadOff = 4, kMOutOff = 6, kMTotal = 8, kMRethLen = 9, kMPmtu = 10,
+    kMRkey = 11, kMDqpn = 12, kMPsn = 13, kMSrcIp = 14, kMDstIp = 15, kMFirst = 16, kMNpk = 17, kMSlot = 18,
+    kMMsnId = 19, kMKind = 20, kMsgDwords = 22
+};
+static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout");
+
+__device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t nmsgs, int idx, MsgRegs &m,
+                                          uint32_t lane) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(msgs + idx);
+    m.v = (lane < static_cast<uint32_t>(kMsgDwords) && static_cast<uint32_t>(idx) < nmsgs) ? w[lane] : 0u;
+    m.idx = idx;
+}
+
+__device__ __forceinline__ void seg_info(const MsgRegs &m, uint32_t s, SegInfo &g) {
+    const uint32_t total = msg_u32(m, kMTotal), pmtu = msg_u32(m, kMPmtu);
+    const uint32_t lva = static_cast<uint32_t>(msg_u64(m, kMLocalVa));
+    uint32_t first = pmtu - lva % pmtu;
+    first = total < first ? total : first;
+    if (s == 0) {
+        g.start = 0;
+        g.len = first;
+    } else {
+        g.start = first + (s - 1) * pmtu;
+        const uint32_t rem = total - g.start;
+        g.len = rem < pmtu ? rem : pmtu;
+    }
+    g.pad = (4u - (g.len & 3u)) & 3u;
+    g.L = 56u + g.len + g.pad + 4u;
+    g.out = msg_u64(m, kMOutOff) + static_cast<uint64_t>(s) * msg_u32(m, kMSlot);
+    g.src = msg_u64(m, kMPayloadOff) + g.start;
+    const int N = 1 + static_cast<int>((g.L - 4u) >> 2);
+    g.R = (N + 63) >> 6;
+    g.k0 = N - 64 * g.R;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+// IPv4 (write_ip_udp_header, packet_processor.rs:307-332) + UDP + BTH (set_from_common_meta,
+// packet.rs:145-153 on a zeroed buffer) + RETH (197-201).
+__device__ __forceinline__ void build_header(const MsgRegs &m, uint32_t s, const SegInfo &g, PacketHdr &h) {
+    const uint32_t n = msg_u32(m, kMNpk);
+    const uint32_t kind = msg_u32(m, kMKind) & 0xffu, tran = (msg_u32(m, kMKind) >> 8) & 0xffu;
+    const bool only = n == 1u, last = s + 1u == n;
+    uint32_t op;
+    if (kind == 0u) op = only ? 0x0Au : (s == 0u ? 0x06u : (last ? 0x08u : 0x07u));
+    else op = only ? 0x10u : (s == 0u ? 0x0Du : (last ? 0x0Fu : 0x0Eu));
+    const uint32_t ack = (only || last) ? 1u : 0u;
+    const uint32_t msn_id = msg_u32(m, kMMsnId), msn = msn_id & 0xffffu, ipid = msn_id >> 16;
+    const uint32_t psn = (msg_u32(m, kMPsn) + s) & 0xffffffu;
+    const uint64_t va = msg_u64(m, kMRemoteVa) + g.start;
+    h.w[0] = 0x45u | (((g.L >> 8) & 0xffu) << 16) | ((g.L & 0xffu) << 24);
+    h.w[1] = bswap16(ipid);
+    h.w[2] = 0x1140u;  // TTL 64, protocol UDP, checksum 0
+    h.w[3] = bswap32(msg_u32(m, kMSrcIp));
+    h.w[4] = bswap32(msg_u32(m, kMDstIp));
+    h.w[5] = bswap16(4791u) | (bswap16(4791u) << 16);
+    h.w[6] = bswap16(g.L - 20u);
+    h.w[7] = (((tran << 5) & 0xffu) | op) | ((g.pad << 5) << 8) | (bswap16(msn) << 16);
+    h.w[8] = bswap32(msg_u32(m, kMDqpn) & 0xffffffu);
+    h.w[9] = bswap32(psn) | (ack << 7);
+    h.w[10] = bswap32(static_cast<uint32_t>(va >> 32));
+    h.w[11] = bswap32(static_cast<uint32_t>(va));
+    h.w[12] = bswap32(msg_u32(m, kMRkey));
+    h.w[13] = bswap32(msg_u32(m, kMRethLen));
+}
+
+__device__ __forceinline__ uint32_t header_word(const PacketHdr &h, int pw) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) v = (pw == i) ? h.w[i] : v;
+    return v;
+}
+
+// Word pw of the packet for the byte-wise path: header, payload bytes from d_src, zero pad.
+__device__ __forceinline__ uint32_t packet_word_bytes(const PacketHdr &h, const uint8_t *src, uint64_t src_bytes,
+                                                      const SegInfo &g, int pw) {
+    if (pw < 0) return 0u;
+    if (pw < 14) return header_word(h, pw);
+    uint32_t w = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t q = 4u * static_cast<uint32_t>(pw) + t - 56u;
+        const uint64_t a = g.src + q;
+        const uint32_t b = (q < g.len && a < src_bytes) ? src[a] : 0u;
+        w |= b << (8 * t);
+    }
+    return w;
+}
+
+template <int RD>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const uint8_t *src, uint64_t src_bytes,
+                                                                          const icrc_write_msg *msgs, uint32_t nmsgs,
+                                                                          uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
+                                                                          uint32_t *pkt_len,
+                                                                          uint32_t *icrc_out, const uint32_t *table) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = t4[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
+    c.fin = kFinalBase + lane * 4u;
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t chunk = ((npk + tw - 1) / tw + 63u) & ~63u;
+    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    if (lo64 >= npk) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t hi = (npk - lo) < chunk ? npk : lo + chunk;
+
+    // message holding packet lo: binary search on first_packet
+    int mlo = 0, mhi = static_cast<int>(nmsgs) - 1;
+    while (mlo < mhi) {
+        const int mid = (mlo + mhi + 1) >> 1;
+        if (msgs[mid].first_packet <= lo) mlo = mid;
+        else mhi = mid - 1;
+    }
+    mlo = __builtin_amdgcn_readfirstlane(mlo);
+
+    // cursors: packet index, its message (one dword per lane), segment, row
+    struct Cur {
+        uint32_t pk;
+        MsgRegs m;
+        SegInfo g;
+        int j;
+        bool fast, fits;
+    };
+    Cur lc, pc;
+    // cur.fits: the packet has a message, a non-zero pmtu, its payload inside d_src and its slot
+    // inside d_wire; cur.fast: it fits and both payload and slot are 4-byte aligned.
+    auto locate = [&](Cur &cur, uint32_t pk) __attribute__((always_inline)) {
+        cur.pk = pk;
+        cur.j = 0;
+        cur.fast = cur.fits = false;
+        cur.g.R = 0;
+        cur.g.L = 0;
+        cur.g.k0 = 0;
+        cur.g.src = 0;
+        cur.g.out = 0;
+        cur.g.len = 0;
+        if (pk >= hi) return;
+        while (cur.m.idx < static_cast<int>(nmsgs) &&
+               (cur.m.idx < 0 || pk >= msg_u32(cur.m, kMFirst) + msg_u32(cur.m, kMNpk))) {
+            const int next = cur.m.idx < 0 ? mlo : cur.m.idx + 1;
+            msg_fetch(msgs, nmsgs, next, cur.m, lane);
+        }
+        if (cur.m.idx >= static_cast<int>(nmsgs) || pk < msg_u32(cur.m, kMFirst) || msg_u32(cur.m, kMPmtu) == 0u)
+            return;
+        SegInfo g;
+        seg_info(cur.m, pk - msg_u32(cur.m, kMFirst), g);
+        cur.fits = g.len <= src_bytes && g.src <= src_bytes - g.len && g.L <= wire_bytes &&
+                   g.out <= wire_bytes - g.L && g.len <= 0x10000u;
+        if (!cur.fits) return;
+        cur.fast = ((reinterpret_cast<uintptr_t>(src) + g.src) & 3u) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(wire) + g.out) & 3u) == 0;
+        cur.g = g;
+    };
+    auto advance = [&](Cur &cur) __attribute__((always_inline)) {  // next packet taking the fast path
+        uint32_t pk = cur.pk + 1u;
+        for (;;) {
+            locate(cur, pk);
+            if (pk >= hi || cur.fast) return;
+            ++pk;
+        }
+    };
+    lc.m.idx = pc.m.idx = -1;
+    lc.m.v = pc.m.v = 0;
+    bool slow_seen = false;
+    locate(lc, lo);
+    if (!lc.fast) advance(lc);
+    locate(pc, lo);
+    if (!pc.fast) {
+        slow_seen = pc.pk < hi;
+        advance(pc);
+    }
+
+    ResultBuf rb_len, rb_crc;
+    rb_len.v = rb_crc.v = 0;
+    rb_len.valid = rb_crc.valid = 0;
+    int rb_block = -1;
+    auto record = [&](uint32_t pk, uint32_t L, uint32_t crc) __attribute__((always_inline)) {
+        const int blk = static_cast<int>(pk >> 6);
+        if (blk != rb_block) {
+            if (rb_len.valid) {
+                const uint32_t base = static_cast<uint32_t>(rb_block) * 64u + lane;
+                if ((rb_len.valid >> lane) & 1ull) {
+                    if (pkt_len) pkt_len[base] = rb_len.v;
+                    if (icrc_out) icrc_out[base] = rb_crc.v;
+                }
+                rb_len.valid = rb_crc.valid = 0;
+            }
+            rb_block = blk;
+        }
+        rb_put(rb_len, pk, L);
+        rb_put(rb_crc, pk, crc);
+    };
+
+    auto load_row = [&](uint32_t &dst) __attribute__((always_inline)) {
+        const int nrec = lc.g.R > 0 ? static_cast<int>((lc.g.len + 3u) & ~3u) : 0;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(src) + (lc.g.R > 0 ? lc.g.src : 0), 0, nrec, 0x00020000);
+        // payload byte offset of this lane's word: 4 * pw - 56 (negative -> out of range -> 0)
+        const uint32_t voff = 4u * static_cast<uint32_t>(lc.g.k0 - 1 + static_cast<int>(lane) + 64 * lc.j) - 56u;
+        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, 0);
+        if (lc.g.R > 0) {
+            lc.j += 1;
+            if (lc.j == lc.g.R) advance(lc);
+        }
+    };
+
+    constexpr int kRD = RD;
+    uint32_t ring[kRD];
+    static_for<kRD>([&](auto ic) __attribute__((always_inline)) -> bool {
+        load_row(ring[decltype(ic)::value]);
+        return true;
+    });
+    PacketHdr h;
+    if (pc.pk < hi) build_header(pc.m, pc.pk - msg_u32(pc.m, kMFirst), pc.g, h);
+    uint32_t acc = 0;
+    while (pc.pk < hi) {
+        static_for<kRD>([&](auto ic) __attribute__((always_inline)) -> bool {
+            constexpr int i = decltype(ic)::value;
+            if (pc.pk >= hi) return false;
+            const int pw = pc.g.k0 - 1 + static_cast<int>(lane) + 64 * pc.j;
+            uint32_t w = ring[i];
+            // last payload word: keep only the payload bytes (pad and garbage -> 0)
+            const int room = static_cast<int>(56u + pc.g.len) - 4 * pw;  // payload bytes from this word on
+            if (room < 4) w = room <= 0 ? 0u : (w & ((1u << (8 * room)) - 1u));
+            if (pc.j < 2) {
+                if (pw >= 0 && pw < 14) w = header_word(h, pw);
+            }
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(wire + pc.g.out, 0,
+                                                                                static_cast<int>(pc.g.L - 4u), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(w, os, static_cast<int>(4u * static_cast<uint32_t>(pw)), 0, 0);
+            uint32_t u = w;
+            if (pc.j < 2) u |= head_mask(pw + 1);
+            if (pc.j == 0) acc = u;
+            else acc = step_m64(lds, acc, u, c);
+            pc.j += 1;
+            if (pc.j == pc.g.R) {
+                const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
+                if (lane == 0) *reinterpret_cast<uint32_t *>(wire + pc.g.out + pc.g.L - 4u) = crc;
+                record(pc.pk, pc.g.L, crc);
+                const uint32_t before = pc.pk;
+                advance(pc);
+                if (pc.pk != before + 1u && before + 1u < hi) slow_seen = true;
+                if (pc.pk < hi) build_header(pc.m, pc.pk - msg_u32(pc.m, kMFirst), pc.g, h);
+            }
+            load_row(ring[i]);
+            return true;
+        });
+    }
+    if (rb_len.valid && (rb_len.valid >> lane) & 1ull) {
+        const uint32_t base = static_cast<uint32_t>(rb_block) * 64u + lane;
+        if (pkt_len) pkt_len[base] = rb_len.v;
+        if (icrc_out) icrc_out[base] = rb_crc.v;
+    }
+
+    // Byte-wise path for packets whose payload or slot is not 4-byte aligned; packets that do not
+    // fit (no message, payload outside d_src, slot outside d_wire) report length 0.
+    if (slow_seen) {
+        Cur sc;
+        sc.m.idx = -1;
+        sc.m.v = 0;
+        for (uint32_t pk = lo; pk < hi; ++pk) {
+            locate(sc, pk);
+            if (sc.fast) continue;
+            if (!sc.fits) {
+                if (lane == 0) {
+                    if (pkt_len) pkt_len[pk] = 0u;
+                    if (icrc_out) icrc_out[pk] = 0u;
+                }
+                continue;
+            }
+            PacketHdr hs;
+            build_header(sc.m, pk - msg_u32(sc.m, kMFirst), sc.g, hs);
+            uint8_t *out = wire + sc.g.out;
+            uint32_t a = 0;
+            for (int r = 0; r < sc.g.R; ++r) {
+                const int pw = sc.g.k0 - 1 + static_cast<int>(lane) + 64 * r;
+                const uint32_t w = packet_word_bytes(hs, src, src_bytes, sc.g, pw);
+                if (pw >= 0 && static_cast<uint32_t>(4 * pw) < sc.g.L - 4u) {
+                    out[4 * pw] = static_cast<uint8_t>(w);
+                    out[4 * pw + 1] = static_cast<uint8_t>(w >> 8);
+                    out[4 * pw + 2] = static_cast<uint8_t>(w >> 16);
+                    out[4 * pw + 3] = static_cast<uint8_t>(w >> 24);
+                }
+                uint32_t u = w;
+                if (r < 2) u |= head_mask(pw + 1);
+                a = (r == 0) ? u : step_m64(lds, a, u, c);
+            }
+            const uint32_t crc = ~wave_xor(final_mul(lds, a, c.fin));
+            if (lane == 0) {
+                uint8_t *t = out + sc.g.L - 4u;
+                t[0] = static_cast<uint8_t>(crc);
+                t[1] = static_cast<uint8_t>(crc >> 8);
+                t[2] = static_cast<uint8_t>(crc >> 16);
+                t[3] = static_cast<uint8_t>(crc >> 24);
+                if (pkt_len) pkt_len[pk] = sc.g.L;
+                if (icrc_out) icrc_out[pk] = crc;
+            }
+        }
+    }
+}
+
 // ---- packet synthesis ----------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -806,6 +1147,15 @@ int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr,
     const uint32_t grid = n < 65536u ? n : 65536u;
     hipLaunchKernelGGL(icrc_synth_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                        base, desc, hdr, n);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
+    if (p.npackets == 0) return ICRC_OK;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((icrc_packetize_kernel<16>), dim3(grid), dim3(kThreadsPerGroup), 0,
+                       static_cast<hipStream_t>(stream), p.src, p.src_bytes, p.msgs, p.nmsgs, p.npackets, p.wire,
+                       p.wire_bytes, p.pkt_len, p.icrc, p.table);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -88,6 +88,18 @@ SYNTH_DESC_DTYPE = np.dtype([
 ])
 assert SYNTH_DESC_DTYPE.itemsize == ctypes.sizeof(SynthDesc) == 40
 
+# icrc_write_msg (include/icrc.h): one RDMA WRITE / READ RESPONSE message for the packetizer.
+WRITE_MSG_DTYPE = np.dtype([
+    ("local_va", "<u8"), ("remote_va", "<u8"), ("payload_offset", "<u8"), ("out_offset", "<u8"),
+    ("total_len", "<u4"), ("reth_len", "<u4"), ("pmtu", "<u4"), ("rkey", "<u4"), ("dqpn", "<u4"),
+    ("psn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("first_packet", "<u4"),
+    ("npackets", "<u4"), ("slot_stride", "<u4"), ("msn", "<u2"), ("ip_id", "<u2"),
+    ("kind", "u1"), ("tran_type", "u1"), ("_pad", "u1", (6,)),
+])
+assert WRITE_MSG_DTYPE.itemsize == 88
+MSG_WRITE, MSG_READ_RESPONSE = 0, 1
+EMULATOR_SRC_IP = 0xC0A80002  # 192.168.0.2, hard-coded in send_write_message (common.rs:124)
+
 
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
@@ -125,6 +137,9 @@ def _load() -> ctypes.CDLL:
                                             ctypes.c_uint16, ctypes.c_uint16]),
         "icrc_rdma_header_len": (i32, [ctypes.c_uint8]),
         "icrc_table_image": (i32, [vp, u32]),
+        "icrc_write_segment_count": (u32, [u64, u32, u32]),
+        "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
+        "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -346,6 +361,51 @@ class Engine:
                                          lens.ctypes.data, off.size, out.ctypes.data,
                                          1 if write_trailer else 0), "icrc_compute_batch_ex")
         return out
+
+    def packetize(self, d_src: int, src_bytes: int, d_msgs: int, nmsgs: int, npackets: int,
+                  d_wire: int, wire_bytes: int, d_pkt_len: int = 0, d_icrc: int = 0,
+                  stream: Optional[int] = None) -> None:
+        """Fused send step (icrc_write_packetize_device): segment, serialise, copy, pad, ICRC."""
+        _check(lib.icrc_write_packetize_device(self.handle, d_src or None, src_bytes, d_msgs, nmsgs,
+                                               npackets, d_wire, wire_bytes, d_pkt_len or None,
+                                               d_icrc or None, stream or None),
+               "icrc_write_packetize_device")
+
+
+def write_segment_count(local_va: int, total_len: int, pmtu: int) -> int:
+    """generate_segments_from_request(...).len() (common.rs:152-176)."""
+    return int(lib.icrc_write_segment_count(local_va, total_len, pmtu))
+
+
+def write_packet_len(local_va: int, total_len: int, pmtu: int, s: int) -> int:
+    """Wire length of segment s of a WRITE / READ RESPONSE message (0 past the last)."""
+    return int(lib.icrc_write_packet_len(local_va, total_len, pmtu, s))
+
+
+def write_messages(specs, slot_stride: int = 0, base_out: int = 0) -> np.ndarray:
+    """Build an icrc_write_msg array from dicts (local_va, remote_va, payload_offset,
+    total_len, pmtu, ...), filling first_packet / npackets / out_offset so the messages' packets
+    are laid out back to back (slot_stride 0 = each message's pmtu + 64, 4-byte aligned)."""
+    msgs = np.zeros(len(specs), dtype=WRITE_MSG_DTYPE)
+    first, out = 0, base_out
+    for i, s in enumerate(specs):
+        m = msgs[i]
+        for k, v in s.items():
+            m[k] = v
+        if "src_ip" not in s:
+            m["src_ip"] = EMULATOR_SRC_IP
+        if "reth_len" not in s:
+            m["reth_len"] = s["total_len"]
+        if "ip_id" not in s:
+            m["ip_id"] = 1  # generate_payload_from_msg (net/util.rs:179)
+        n = write_segment_count(int(s.get("local_va", 0)), int(s["total_len"]), int(s["pmtu"]))
+        stride = int(s.get("slot_stride", slot_stride or ((int(s["pmtu"]) + 64 + 3) & ~3)))
+        m["npackets"], m["first_packet"], m["slot_stride"] = n, first, stride
+        if "out_offset" not in s:
+            m["out_offset"] = out
+        out = int(m["out_offset"]) + n * stride
+        first += n
+    return msgs
 
 
 from . import workloads  # noqa: E402,F401  (synthetic packet streams, SURVEY §8d)

@@ -242,6 +242,63 @@ def synth_write(total_len: int, pmtu: int, *, local_va: int, remote_va: int, rke
     return buf, off, lens
 
 
+_SEND_OPCODES = {  # (only, first, middle, last): write.rs:31-96, read_response.rs:30-95
+    0: (0x0A, 0x06, 0x07, 0x08),
+    1: (0x10, 0x0D, 0x0E, 0x0F),
+}
+
+
+def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
+    """The emulator's send step for an icrc_write_msg array (fields as in include/icrc.h):
+    per message generate_segments_from_request (common.rs:152-176), per segment the Write /
+    ReadResponse handler's opcode / PSN / ack_req / RETH choice and send_write_message
+    (common.rs:73-132) -> generate_payload_from_msg -> PacketWriter::write with the ICRC
+    trailer.  Returns (wire, pkt_len, icrc) with packets at out_offset + s * slot_stride."""
+    wire = np.zeros(wire_bytes, dtype=np.uint8)
+    npk = int(msgs["npackets"].sum()) if len(msgs) else 0
+    lens = np.zeros(npk, dtype=np.uint32)
+    icrcs = np.zeros(npk, dtype=np.uint32)
+    for m in msgs:
+        segs = generate_segments(int(m["local_va"]), int(m["total_len"]), int(m["pmtu"]))
+        assert len(segs) == int(m["npackets"])
+        only, first, middle, last = _SEND_OPCODES[int(m["kind"])]
+        pos = 0
+        for s, (_, sl) in enumerate(segs):
+            if len(segs) == 1:
+                op, ack = only, 1
+            elif s == 0:
+                op, ack = first, 0
+            elif s + 1 == len(segs):
+                op, ack = last, 1
+            else:
+                op, ack = middle, 0
+            po = int(m["payload_offset"]) + pos
+            payload = np.ascontiguousarray(src[po: po + sl])
+            msg = RdmaMsg()
+            msg.kind = 0
+            msg.opcode = op
+            msg.tran_type = int(m["tran_type"])
+            msg.ack_req = ack
+            msg.pkey = int(m["msn"])
+            msg.dqpn = int(m["dqpn"])
+            msg.psn = (int(m["psn"]) + s) & 0xFFFFFFFF
+            msg.reth_va = (int(m["remote_va"]) + pos) & 0xFFFFFFFFFFFFFFFF
+            msg.reth_rkey = int(m["rkey"])
+            msg.reth_len = int(m["reth_len"])
+            msg.payload = payload.ctypes.data if sl else None
+            msg.payload_len = sl
+            rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]))
+            if rc:
+                raise ValueError(f"packet_write rc={rc}")
+            icrc = int(pkt[-4:].view("<u4")[0])
+            o = int(m["out_offset"]) + s * int(m["slot_stride"])
+            wire[o: o + pkt.size] = pkt
+            k = int(m["first_packet"]) + s
+            lens[k], icrcs[k] = pkt.size, icrc
+            pos += sl
+    return wire, lens, icrcs
+
+
 def synth_middle_stream(n: int, *, pmtu: int = 4096, stride: int | None = None,
                         remote_va: int = 0x7F7E8FC00000, reth_len: int = 0, rkey: int = 0x2000003,
                         dqpn: int = 2, psn0: int = 0, msn: int = 0, dst_ip: int = 0xC0A80003,

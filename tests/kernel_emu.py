@@ -58,6 +58,53 @@ def stream_words(pkt: np.ndarray, z: int, k: np.ndarray) -> np.ndarray:
     return out
 
 
+def _bswap32(x: int) -> int:
+    return int.from_bytes((x & 0xFFFFFFFF).to_bytes(4, "little"), "big")
+
+
+def _bswap16(x: int) -> int:
+    return ((x & 0xFF) << 8) | ((x >> 8) & 0xFF)
+
+
+def packetizer_header_words(m, s: int) -> tuple:
+    """icrc_packetize_kernel's seg_info + build_header for segment s of message m (a
+    WRITE_MSG_DTYPE record): returns (14 LE header words, payload len, wire length L)."""
+    total, pmtu = int(m["total_len"]), int(m["pmtu"])
+    first = min(total, pmtu - (int(m["local_va"]) & 0xFFFFFFFF) % pmtu)
+    if s == 0:
+        start, ln = 0, first
+    else:
+        start = first + (s - 1) * pmtu
+        ln = min(pmtu, total - start)
+    pad = (4 - (ln & 3)) & 3
+    L = 56 + ln + pad + 4
+    n = int(m["npackets"])
+    only, last = n == 1, s + 1 == n
+    if int(m["kind"]) == 0:
+        op = 0x0A if only else (0x06 if s == 0 else (0x08 if last else 0x07))
+    else:
+        op = 0x10 if only else (0x0D if s == 0 else (0x0F if last else 0x0E))
+    ack = 1 if (only or last) else 0
+    psn = (int(m["psn"]) + s) & 0xFFFFFF
+    va = (int(m["remote_va"]) + start) & 0xFFFFFFFFFFFFFFFF
+    w = [0] * 14
+    w[0] = 0x45 | (((L >> 8) & 0xFF) << 16) | ((L & 0xFF) << 24)
+    w[1] = _bswap16(int(m["ip_id"]))
+    w[2] = 0x1140
+    w[3] = _bswap32(int(m["src_ip"]))
+    w[4] = _bswap32(int(m["dst_ip"]))
+    w[5] = _bswap16(4791) | (_bswap16(4791) << 16)
+    w[6] = _bswap16(L - 20)
+    w[7] = (((int(m["tran_type"]) << 5) & 0xFF) | op) | ((pad << 5) << 8) | (_bswap16(int(m["msn"])) << 16)
+    w[8] = _bswap32(int(m["dqpn"]) & 0xFFFFFF)
+    w[9] = _bswap32(psn) | (ack << 7)
+    w[10] = _bswap32(va >> 32)
+    w[11] = _bswap32(va & 0xFFFFFFFF)
+    w[12] = _bswap32(int(m["rkey"]))
+    w[13] = _bswap32(int(m["reth_len"]))
+    return tuple(w), ln, L
+
+
 def icrc(img: np.ndarray, pkt: np.ndarray) -> int:
     Ld = pkt.size - 4
     T = 4 + Ld

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 24, names
+    assert len(names) == 27, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -189,3 +189,59 @@ def test_workload_c2_mixed_shape():
     assert 0.07 < float(np.mean(w.desc["payload_len"] % 4 != 0) + np.mean(
         (pl != 256) & (pl != 1024) & (pl != 4096) & (pl % 4 == 0))) < 0.13
     assert np.all(w.off[1:] >= w.off[:-1] + w.lens[:-1])
+
+
+def test_write_segmentation_matches_oracle():
+    import icrc_amd
+
+    rng = np.random.default_rng(5)
+    cases = [(0, 0, 4096), (0, 1, 256), (4095, 2, 4096), (0x7F7E8EE00100, 20000, 4096),
+             (0x1000, 4096, 4096), (0x1001, 4096, 4096), (7, 1 << 24, 256)]
+    cases += [(int(rng.integers(0, 1 << 48)), int(rng.integers(0, 70000)),
+               int(rng.choice([256, 512, 1024, 2048, 4096]))) for _ in range(200)]
+    for va, ln, pmtu in cases:
+        segs = oracle.generate_segments(va, ln, pmtu)
+        assert icrc_amd.write_segment_count(va, ln, pmtu) == len(segs), (va, ln, pmtu)
+        for s in (0, 1, len(segs) // 2, len(segs) - 1):
+            if s < len(segs):
+                sl = segs[s][1]
+                assert icrc_amd.write_packet_len(va, ln, pmtu, s) == 56 + sl + (-sl % 4) + 4
+        assert icrc_amd.write_packet_len(va, ln, pmtu, len(segs)) == 0
+    assert icrc_amd.write_segment_count(0, 100, 0) == 0
+
+
+def _packetizer_specs(rng):
+    return [
+        dict(local_va=0x7F7E8EE00100, remote_va=0x7F7E8FC00000, payload_offset=0, total_len=20000,
+             pmtu=4096, rkey=0x2000003, dqpn=2, psn=0, msn=0, dst_ip=0xC0A80003, kind=0),
+        dict(local_va=0x1000, remote_va=0xFFFFFFFFFFFFF000, payload_offset=20000, total_len=3,
+             pmtu=256, rkey=1, dqpn=0x1FFFFFF, psn=0xFFFFFF, msn=0xBEEF, dst_ip=0x0A000001, kind=1),
+        dict(local_va=0x2000, remote_va=0x10, payload_offset=20004, total_len=0, pmtu=1024, rkey=7,
+             dqpn=3, psn=5, msn=1, dst_ip=0x0A000002, kind=0, ip_id=0x1234, tran_type=0),
+        dict(local_va=0x3FF, remote_va=0x1234567, payload_offset=20008, total_len=5000, pmtu=1024,
+             rkey=0xFFFFFFFF, dqpn=9, psn=0xFFFFFE, msn=0xFFFF, dst_ip=0xC0A80004, kind=1,
+             reth_len=123456789),
+    ]
+
+
+def test_packetizer_header_formulas_match_oracle():
+    """The kernel's per-word header formulas (kernel_emu.packetizer_header_words) give the bytes
+    the oracle's PacketWriter restatement writes, for WRITE and READ RESPONSE messages."""
+    import icrc_amd
+
+    rng = np.random.default_rng(11)
+    msgs = icrc_amd.write_messages(_packetizer_specs(rng))
+    src = rng.integers(0, 256, 30000, dtype=np.uint8)
+    wire_bytes = int(msgs["out_offset"][-1]) + int(msgs["npackets"][-1]) * int(msgs["slot_stride"][-1])
+    wire, lens, icrcs = oracle.send_messages(src, msgs, wire_bytes)
+    for m in msgs:
+        for s in range(int(m["npackets"])):
+            words, ln, L = kernel_emu.packetizer_header_words(m, s)
+            k = int(m["first_packet"]) + s
+            assert L == lens[k]
+            o = int(m["out_offset"]) + s * int(m["slot_stride"])
+            hdr = np.array(words, dtype="<u4").view(np.uint8)
+            np.testing.assert_array_equal(hdr, wire[o: o + 56])
+            pkt = wire[o: o + L]
+            assert np.all(pkt[56 + ln: L - 4] == 0)
+            assert oracle.compute_icrc(pkt) == icrcs[k]

@@ -319,3 +319,135 @@ def test_full_size_c1_properties(engine, n):
     np.testing.assert_array_equal(
         d_out.cpu().numpy().view(np.uint32)[idx],
         oracle_icrcs(host, idx.astype(np.uint64) * np.uint64(L), np.full(idx.size, L, np.uint32)))
+
+
+# ---- fused send packetizer (icrc_write_packetize_device) vs the oracle's send path ----------
+def run_packetize(engine, src: np.ndarray, msgs: np.ndarray, wire_bytes: int, fill: int = 0):
+    import icrc_amd
+
+    npk = int(msgs["npackets"].sum())
+    d_src = dev(src)
+    d_msgs = dev(msgs.view(np.uint8))
+    d_wire = torch.full((wire_bytes,), fill, dtype=torch.uint8, device="cuda")
+    d_len = torch.full((npk,), -1, dtype=torch.int32, device="cuda")
+    d_icrc = torch.zeros(npk, dtype=torch.int32, device="cuda")
+    engine.packetize(d_src.data_ptr(), src.size, d_msgs.data_ptr(), len(msgs), npk, d_wire.data_ptr(),
+                     wire_bytes, d_len.data_ptr(), d_icrc.data_ptr(), stream=stream_handle())
+    torch.cuda.synchronize()
+    return (d_wire.cpu().numpy(), d_len.cpu().numpy().view(np.uint32), d_icrc.cpu().numpy().view(np.uint32))
+
+
+def _random_specs(rng, nmsg, aligned=True):
+    specs, off = [], 0
+    for i in range(nmsg):
+        pmtu = int(rng.choice([256, 512, 1024, 2048, 4096]))
+        ln = int(rng.choice([0, 1, 3, 4, 255, 256, 257, pmtu, pmtu + 1, 3 * pmtu + 7,
+                             int(rng.integers(0, 20000))]))
+        lva = int(rng.integers(0, 1 << 47))
+        if aligned:
+            off = (off + 3) & ~3
+            lva &= ~3
+        specs.append(dict(local_va=lva, remote_va=int(rng.integers(0, 1 << 64, dtype=np.uint64)),
+                          payload_offset=off, total_len=ln, pmtu=pmtu, rkey=int(rng.integers(0, 1 << 32)),
+                          dqpn=int(rng.integers(0, 1 << 24)), psn=int(rng.integers(0, 1 << 24)),
+                          msn=int(rng.integers(0, 1 << 16)), dst_ip=int(rng.integers(0, 1 << 32)),
+                          kind=int(rng.integers(0, 2)), ip_id=int(rng.integers(0, 1 << 16))))
+        off += ln + int(rng.integers(0, 8))
+    return specs, off
+
+
+@pytest.mark.parametrize("layout", ["aligned", "mixed", "odd_slots"])
+def test_packetize_matches_oracle(engine, layout):
+    """aligned: every packet on the word path; mixed: payloads at odd offsets (word path and
+    byte path interleaved in one wave); odd_slots: every slot misaligned (byte path)."""
+    import icrc_amd
+
+    rng = np.random.default_rng({"aligned": 21, "mixed": 22, "odd_slots": 23}[layout])
+    specs, src_bytes = _random_specs(rng, 40, layout == "aligned")
+    msgs = icrc_amd.write_messages(specs, slot_stride=4163 if layout == "odd_slots" else 0)
+    if layout == "odd_slots":
+        msgs["out_offset"] += 1
+    src = rng.integers(0, 256, src_bytes + 16, dtype=np.uint8)
+    wire_bytes = int(msgs["out_offset"][-1]) + int(msgs["npackets"][-1]) * int(msgs["slot_stride"][-1]) + 64
+    want, wl, wi = oracle.send_messages(src, msgs, wire_bytes)
+    got, gl, gi = run_packetize(engine, src, msgs, wire_bytes)
+    np.testing.assert_array_equal(gl, wl)
+    np.testing.assert_array_equal(gi, wi)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_packetize_reference_write_path(engine):
+    """C3: one 20000-byte WRITE from local_va 0x..100 equals oracle.synth_write."""
+    import icrc_amd
+
+    total, pmtu, lva = 20000, 4096, 0x7F7E8EE00100
+    ref, off, lens = oracle.synth_write(total, pmtu, local_va=lva, remote_va=0x7F7E8FC00000, rkey=0x2000003,
+                                        dqpn=2, psn0=0, msn=0, dst_ip=0xC0A80003, payload_key=0xABCDEF)
+    src = np.array([(oracle.mix64(0xABCDEF + (q >> 3)) >> (8 * (q & 7))) & 0xFF for q in range(total)],
+                   dtype=np.uint8)
+    stride = int(off[1] - off[0])
+    msgs = icrc_amd.write_messages([dict(local_va=lva, remote_va=0x7F7E8FC00000, payload_offset=0,
+                                         total_len=total, pmtu=pmtu, rkey=0x2000003, dqpn=2, psn=0, msn=0,
+                                         dst_ip=0xC0A80003, kind=0)], slot_stride=stride)
+    got, gl, gi = run_packetize(engine, src, msgs, ref.size)
+    np.testing.assert_array_equal(gl, lens)
+    for i in range(len(lens)):
+        np.testing.assert_array_equal(got[int(off[i]): int(off[i]) + int(lens[i])],
+                                      ref[int(off[i]): int(off[i]) + int(lens[i])])
+
+
+def test_packetize_bounds(engine):
+    """Packets whose slot runs past wire_bytes, or whose payload runs past d_src, are not written
+    and report length 0; nothing outside the wire buffer changes."""
+    import icrc_amd
+
+    rng = np.random.default_rng(3)
+    msgs = icrc_amd.write_messages([dict(local_va=0, remote_va=0, payload_offset=0, total_len=4 * 4096,
+                                         pmtu=4096, rkey=1, dqpn=1, psn=0, msn=0, dst_ip=1, kind=0)])
+    stride = int(msgs["slot_stride"][0])
+    src = rng.integers(0, 256, 4 * 4096, dtype=np.uint8)
+    wire_bytes = 3 * stride + 100  # the 4th packet does not fit
+    want, wl, wi = oracle.send_messages(src, msgs, 4 * stride)
+    got, gl, gi = run_packetize(engine, src, msgs, wire_bytes, fill=0xAB)
+    assert gl.tolist()[:3] == wl.tolist()[:3] and gl[3] == 0 and gi[3] == 0
+    for i in range(3):
+        np.testing.assert_array_equal(got[i * stride: i * stride + int(wl[i])], want[i * stride: i * stride + int(wl[i])])
+    assert np.all(got[3 * stride:] == 0xAB)
+    # payload short by one byte: the last packet is refused, earlier ones are exact
+    got, gl, gi = run_packetize(engine, src[:-1].copy(), msgs, 4 * stride)
+    assert gl.tolist()[:3] == wl.tolist()[:3] and gl[3] == 0
+
+
+def test_packetize_full_message_roundtrip(engine):
+    """A 64 MiB READ RESPONSE at 4 KiB MTU (16384 packets): every packet verifies on the GPU,
+    and a sample of packets equals the oracle's bytes."""
+    import icrc_amd
+
+    total, pmtu = 64 << 20, 4096
+    rng = np.random.default_rng(9)
+    msgs = icrc_amd.write_messages([dict(local_va=0x10000, remote_va=0x7F0000000000, payload_offset=0,
+                                         total_len=total, pmtu=pmtu, rkey=5, dqpn=6, psn=0xFFFF00, msn=2,
+                                         dst_ip=0xC0A80003, kind=1)])
+    npk = int(msgs["npackets"][0])
+    stride = int(msgs["slot_stride"][0])
+    src = rng.integers(0, 256, total, dtype=np.uint8)
+    d_src = dev(src)
+    d_msgs = dev(msgs.view(np.uint8))
+    d_wire = torch.zeros(npk * stride, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(npk, dtype=torch.int32, device="cuda")
+    engine.packetize(d_src.data_ptr(), total, d_msgs.data_ptr(), 1, npk, d_wire.data_ptr(), npk * stride,
+                     d_len.data_ptr(), 0, stream=stream_handle())
+    d_ok = torch.zeros(npk, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(npk, dtype=torch.int64, device="cuda") * stride
+    engine.verify_batch(d_wire.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), npk, d_ok.data_ptr(),
+                        stream=stream_handle())
+    torch.cuda.synchronize()
+    assert int(d_ok.sum()) == npk
+    lens = d_len.cpu().numpy()
+    assert np.all(lens == 56 + pmtu + 4)
+    wire = d_wire.cpu().numpy()
+    sample = [0, 1, npk // 2, npk - 1]
+    sub = msgs.copy()
+    want, wl, _ = oracle.send_messages(src, sub, npk * stride)
+    for i in sample:
+        np.testing.assert_array_equal(wire[i * stride: i * stride + lens[i]], want[i * stride: i * stride + lens[i]])
