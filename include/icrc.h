@@ -117,6 +117,49 @@ int icrc_verify_strided_device(icrc_engine *engine, uint8_t *d_base, uint64_t st
                                uint32_t len, uint32_t n, uint8_t *d_ok, int zero_trailer,
                                void *stream);
 
+/* ---- fused receive: verify + strip + parse (§8f row 2) --------------------------------------
+ * One pass over each received IPv4 packet: is_icrc_valid (packet_processor.rs:341-353), then
+ * PacketProcessor::to_rdma_message (packet_processor.rs:18-71, packet.rs:286-438) applied to the
+ * UDP payload with the ICRC stripped (pkt[28 .. L-4)): the emulator hands the whole datagram,
+ * trailer included, to to_rdma_message (device_inner.rs:150) and so reports payloads 4 bytes
+ * too long; here payload_len excludes it.  The header words are taken from the registers the
+ * ICRC pass already loaded — no second read of the packet. */
+#define ICRC_RX_OK 0u
+#define ICRC_RX_INVALID_OPCODE 1u     /* PacketError::InvalidOpcode (opcode not in 0x06..0x11)   */
+#define ICRC_RX_INVALID_TRANS_TYPE 2u /* PacketError::FailedToConvertTransType (tran_type > 6) */
+#define ICRC_RX_TRUNCATED 3u          /* L < 44, or headers + pad longer than the packet (the
+                                         reference reads out of bounds there)                  */
+#define ICRC_RX_SOLICITED 0x01u
+#define ICRC_RX_ACK_REQ 0x02u
+#define ICRC_RX_HAS_IMM 0x04u
+#define ICRC_RX_HAS_SECONDARY_RETH 0x08u
+#define ICRC_RX_ACKNOWLEDGE 0x10u /* Metadata::Acknowledge (AETH fields valid), else General */
+typedef struct icrc_rx_desc {
+    uint64_t reth_va;        /* RETH (General metadata)                                    */
+    uint64_t sec_va;         /* secondary RETH (RdmaReadRequest)                            */
+    uint64_t payload_offset; /* byte offset of the payload in d_base                        */
+    uint32_t payload_len;    /* UDP payload - ICRC - headers - pad (get_packet_real_length) */
+    uint32_t reth_rkey, reth_len;
+    uint32_t sec_rkey, sec_len;
+    uint32_t imm;
+    uint32_t dqpn, psn;
+    uint32_t aeth_msn;
+    uint16_t pkey;
+    uint8_t opcode, tran_type;
+    uint8_t flags;           /* ICRC_RX_* bits                                               */
+    uint8_t pad_cnt;
+    uint8_t aeth_code, aeth_value;
+    uint8_t icrc_ok;         /* ICRC_VERIFY_OK / _MISMATCH / _BADLEN                          */
+    uint8_t status;          /* ICRC_RX_*; on status != OK every parsed field is 0           */
+    uint8_t _pad[2];
+} icrc_rx_desc; /* 72 bytes */
+/* Packet i = d_base[d_off[i] .. + d_len[i]) (d_off / d_len NULL => i * stride / len).  d_ok
+ * (may be NULL) receives icrc_ok as in icrc_verify_batch_device; zero_trailer as there. */
+int icrc_rx_parse_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d_off,
+                         const uint32_t *d_len, uint64_t stride, uint32_t len, uint32_t n,
+                         icrc_rx_desc *d_desc, uint8_t *d_ok, int zero_trailer, uint32_t *d_nerr,
+                         void *stream);
+
 /* ---- packet synthesis on the device (bench inputs; precursor of the fused packetizer) --- */
 /* Packet i = header template d_hdr[hdr_index*64 .. +hdr_len) ‖ payload ‖ zero pad ‖ zero
  * ICRC slot, written at d_base + offset.  Payload byte q = byte ((pos+q) & 7) of

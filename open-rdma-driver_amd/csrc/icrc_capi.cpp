@@ -497,6 +497,28 @@ int icrc_synth_device(icrc_engine *e, uint8_t *d_base, const icrc_synth_desc *d_
     return icrc::launch_synth(d_base, d_desc, d_hdr, n, stream);
 }
 
+int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                         uint64_t stride, uint32_t len, uint32_t n, icrc_rx_desc *d_desc, uint8_t *d_ok,
+                         int zero_trailer, uint32_t *d_nerr, void *stream) {
+    if (!e || !d_base || !d_desc) return ICRC_EINVAL;
+    if (n == 0) return ICRC_OK;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    BatchParams p{};
+    p.base = d_base;
+    p.off = d_off;
+    p.len = d_len;
+    p.stride = stride;
+    p.ulen = len;
+    p.n = n;
+    p.ok = d_ok;
+    p.nerr = d_nerr;
+    p.table = e->d_table;
+    p.trailer = zero_trailer ? 1 : 0;
+    p.rx = d_desc;
+    return icrc::launch_rx(p, grid_for(e, n), stream);
+}
+
 uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {
     if (pmtu == 0) return 0;
     const uint32_t first = icrc::write_first_segment(local_va, total_len, pmtu);

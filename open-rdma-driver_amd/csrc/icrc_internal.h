@@ -36,6 +36,7 @@ struct BatchParams {
     const uint32_t *table;  // kLdsWords image in device memory
     int trailer;     // compute: write trailer; verify: zero trailer
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
+    icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
 };
 
 constexpr int kDefaultVariant = 1;
@@ -48,6 +49,7 @@ constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
 
 // Launch wrappers (icrc_kernels.hip).  `grid` = number of workgroups.
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
+int launch_rx(const BatchParams &p, int grid, void *stream);  // verify + parse (p.rx)
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {

@@ -229,7 +229,7 @@ __device__ __forceinline__ void store_result(const BatchParams &p, uint32_t i, u
     if (MODE == kCompute) {
         if (p.out) p.out[i] = r;
     } else {
-        p.ok[i] = static_cast<uint8_t>(r);
+        if (p.ok) p.ok[i] = static_cast<uint8_t>(r);
     }
 }
 
@@ -520,7 +520,97 @@ __device__ __forceinline__ void rb_record(const BatchParams &p, ResultBuf &rb, i
     rb_put(rb, q, r);
 }
 
-template <int MODE, int RD>
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+// ---- receive parse (icrc_rx_parse_device) --------------------------------------------------
+// `hdr` holds packet word w (bytes 4w .. 4w+3, LE, zero past L-4) in lane w for w < 18: the
+// IPv4 + UDP + BTH + up to 32 bytes of extension headers.  Restates to_rdma_message
+// (packet_processor.rs:18-71) on the UDP payload with the ICRC stripped; field getters
+// packet.rs:57-98 (BTH), 173-183 (RETH), 222-232 (AETH), 249-251 (Immediate).  Lane k < 18
+// stores dword k of the 72-byte icrc_rx_desc.
+__device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t hdr, uint64_t off, uint32_t L,
+                                         uint32_t icrc_ok, uint32_t lane) {
+    uint32_t f[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) f[k] = 0u;
+    uint32_t status = ICRC_RX_TRUNCATED;
+    if (L >= ICRC_MIN_PACKET) {
+        const uint32_t w7 = __builtin_amdgcn_readlane(hdr, 7);
+        const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+        // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
+        const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                          : (op == 0x0Cu)                 ? 44u
+                          : (op == 0x11u)                 ? 16u
+                          : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                          : 0u;
+        if (hs == 0u) {
+            status = ICRC_RX_INVALID_OPCODE;
+        } else if (tran > 6u) {
+            status = ICRC_RX_INVALID_TRANS_TYPE;
+        } else if (L - 32u < hs + pad) {  // buf_size = L - 28 - 4
+            status = ICRC_RX_TRUNCATED;
+        } else {
+            status = ICRC_RX_OK;
+            const uint32_t w8 = __builtin_amdgcn_readlane(hdr, 8), w9 = __builtin_amdgcn_readlane(hdr, 9);
+            const uint32_t w10 = __builtin_amdgcn_readlane(hdr, 10);
+            uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u);
+            const uint64_t poff = off + 28u + hs;
+            f[4] = static_cast<uint32_t>(poff);
+            f[5] = static_cast<uint32_t>(poff >> 32);
+            f[6] = L - 32u - hs - pad;
+            f[12] = bswap32(w8) & 0xFFFFFFu;
+            f[13] = bswap32(w9) & 0xFFFFFFu;
+            uint32_t code = 0, value = 0;
+            if (hs == 16u) {
+                flags |= ICRC_RX_ACKNOWLEDGE;
+                code = (w10 >> 5) & 3u;
+                value = w10 & 0x1Fu;
+                f[14] = bswap32(w10) & 0xFFFFFFu;
+            } else {
+                const uint32_t w11 = __builtin_amdgcn_readlane(hdr, 11), w12 = __builtin_amdgcn_readlane(hdr, 12);
+                const uint32_t w13 = __builtin_amdgcn_readlane(hdr, 13);
+                f[0] = bswap32(w11);
+                f[1] = bswap32(w10);
+                f[7] = bswap32(w12);
+                f[8] = bswap32(w13);
+                const uint32_t w14 = __builtin_amdgcn_readlane(hdr, 14);
+                if (hs == 32u) {
+                    flags |= ICRC_RX_HAS_IMM;
+                    f[11] = bswap32(w14);
+                } else if (hs == 44u) {
+                    flags |= ICRC_RX_HAS_SECONDARY_RETH;
+                    f[2] = bswap32(__builtin_amdgcn_readlane(hdr, 15));
+                    f[3] = bswap32(w14);
+                    f[9] = bswap32(__builtin_amdgcn_readlane(hdr, 16));
+                    f[10] = bswap32(__builtin_amdgcn_readlane(hdr, 17));
+                }
+            }
+            f[15] = bswap16(w7 >> 16) | (op << 16) | (tran << 24);
+            f[16] = flags | (pad << 8) | (code << 16) | (value << 24);
+        }
+    }
+    f[17] = (icrc_ok & 0xFFu) | (status << 8);
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) v = (lane == static_cast<uint32_t>(k)) ? f[k] : v;
+    if (lane < 18u) reinterpret_cast<uint32_t *>(rx + i)[lane] = v;
+}
+
+// Header words of a packet at any alignment, byte-wise (generic path).
+__device__ __forceinline__ uint32_t rx_header_bytes(const uint8_t *pkt, uint32_t L, uint32_t lane) {
+    uint32_t w = 0;
+    if (lane < 18u && L >= 4u) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t o = 4u * lane + t;
+            w |= (o < L - 4u ? static_cast<uint32_t>(pkt[o]) : 0u) << (8 * t);
+        }
+    }
+    return w;
+}
+
+template <int MODE, int RD, bool PARSE = false>
 __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq) {
     if (nq == 0) return;
@@ -592,6 +682,7 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
                 } else {
                     if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
                     rb_record<MODE>(p, rb, rb_block, lo, cur.q, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN, lane);
+                    if constexpr (PARSE) rx_store(p.rx, lo + cur.q, 0u, off, L, ICRC_VERIFY_BADLEN, lane);
                 }
             }
         }
@@ -621,11 +712,20 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
     });
 
     uint32_t acc = 0;
+    uint32_t hdr = 0;  // PARSE: packet word w in lane w (w < 18), gathered from rows 0 and 1
     while (pc.R > 0) {
         static_for<RD>([&](auto ic) __attribute__((always_inline)) -> bool {
             constexpr int i = decltype(ic)::value;
             if (pc.R == 0) return false;
             uint32_t u = ring[i];
+            if constexpr (PARSE) {
+                if (pc.j < 2) {
+                    const int sl = static_cast<int>(lane) + 1 - pc.k0 - 64 * pc.j;  // lane holding word `lane`
+                    const uint32_t v = static_cast<uint32_t>(
+                        __builtin_amdgcn_ds_bpermute((sl & 63) << 2, static_cast<int>(u)));
+                    hdr = (sl >= 0 && sl < 64) ? v : (pc.j == 0 ? 0u : hdr);
+                }
+            }
             if (pc.j < 2) u |= head_mask(pc.k0 + static_cast<int>(lane) + 64 * pc.j);
             if (pc.j == 0) acc = u;
             else acc = step_m64(lds, acc, u, c);
@@ -634,6 +734,8 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
                 const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
                 const uint32_t r = packet_result<MODE>(p, pc.pkt, pc.L - 4u, crc, true, lane);
                 rb_record<MODE>(p, rb, rb_block, lo, pc.q, r, lane);
+                if constexpr (PARSE)
+                    rx_store(p.rx, lo + pc.q, hdr, static_cast<uint64_t>(pc.pkt - p.base), pc.L, r, lane);
                 next_packet(pc, false);
             }
             load_row(ring[i]);
@@ -660,8 +762,11 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
             uint8_t *pkt = p.base + off;
             int k0 = 0;
             if (classify(pkt, L, k0) < 0) {
+                uint32_t hdr_slow = 0;
+                if constexpr (PARSE) hdr_slow = rx_header_bytes(pkt, L, lane);  // before the trailer is zeroed
                 const uint32_t r = handle_packet<MODE>(p, pkt, L, lds, c, lane);
                 if (lane == 0) store_result<MODE>(p, lo + q, r);
+                if constexpr (PARSE) rx_store(p.rx, lo + q, hdr_slow, off, L, r, lane);
             }
         }
     }
@@ -713,6 +818,31 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
         const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
         run_pipelined<MODE, S, D, ABL>(p, lds, c, lane, lo, nq);
     }
+}
+
+// Receive: verify + strip + parse, the row stream with header capture (RD rows in flight).
+template <int RD>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
+    c.fin = kFinalBase + lane * 4u;
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    if (lo64 >= p.n) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    run_rowstream<kVerify, RD, true>(p, lds, c, lane, lo, nq);
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
@@ -780,8 +910,6 @@ __device__ __forceinline__ void seg_info(const MsgRegs &m, uint32_t s, SegInfo &
     g.k0 = N - 64 * g.R;
 }
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
 
 // IPv4 (write_ip_udp_header, packet_processor.rs:307-332) + UDP + BTH (set_from_common_meta,
 // packet.rs:145-153 on a zeroed buffer) + RETH (197-201).
@@ -1147,6 +1275,13 @@ int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr,
     const uint32_t grid = n < 65536u ? n : 65536u;
     hipLaunchKernelGGL(icrc_synth_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                        base, desc, hdr, n);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_rx(const BatchParams &p, int grid, void *stream) {
+    if (p.n == 0) return ICRC_OK;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((icrc_rx_kernel<16>), dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -98,6 +98,18 @@ WRITE_MSG_DTYPE = np.dtype([
 ])
 assert WRITE_MSG_DTYPE.itemsize == 88
 MSG_WRITE, MSG_READ_RESPONSE = 0, 1
+
+# icrc_rx_desc (include/icrc.h): one parsed received packet.
+RX_DESC_DTYPE = np.dtype([
+    ("reth_va", "<u8"), ("sec_va", "<u8"), ("payload_offset", "<u8"), ("payload_len", "<u4"),
+    ("reth_rkey", "<u4"), ("reth_len", "<u4"), ("sec_rkey", "<u4"), ("sec_len", "<u4"),
+    ("imm", "<u4"), ("dqpn", "<u4"), ("psn", "<u4"), ("aeth_msn", "<u4"), ("pkey", "<u2"),
+    ("opcode", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("pad_cnt", "u1"),
+    ("aeth_code", "u1"), ("aeth_value", "u1"), ("icrc_ok", "u1"), ("status", "u1"),
+    ("_pad", "u1", (2,)),
+])
+assert RX_DESC_DTYPE.itemsize == 72
+RX_OK, RX_INVALID_OPCODE, RX_INVALID_TRANS_TYPE, RX_TRUNCATED = 0, 1, 2, 3
 EMULATOR_SRC_IP = 0xC0A80002  # 192.168.0.2, hard-coded in send_write_message (common.rs:124)
 
 
@@ -140,6 +152,7 @@ def _load() -> ctypes.CDLL:
         "icrc_write_segment_count": (u32, [u64, u32, u32]),
         "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
         "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
+        "icrc_rx_parse_device": (i32, [vp, vp, vp, vp, u64, u32, u32, vp, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -361,6 +374,14 @@ class Engine:
                                          lens.ctypes.data, off.size, out.ctypes.data,
                                          1 if write_trailer else 0), "icrc_compute_batch_ex")
         return out
+
+    def rx_parse(self, d_base: int, d_off: int, d_len: int, n: int, d_desc: int, d_ok: int = 0,
+                 zero_trailer: bool = False, d_nerr: int = 0, stride: int = 0, length: int = 0,
+                 stream: Optional[int] = None) -> None:
+        """Fused receive (icrc_rx_parse_device): verify + strip + parse into RX_DESC_DTYPE."""
+        _check(lib.icrc_rx_parse_device(self.handle, d_base, d_off or None, d_len or None, stride, length, n,
+                                        d_desc, d_ok or None, 1 if zero_trailer else 0, d_nerr or None,
+                                        stream or None), "icrc_rx_parse_device")
 
     def packetize(self, d_src: int, src_bytes: int, d_msgs: int, nmsgs: int, npackets: int,
                   d_wire: int, wire_bytes: int, d_pkt_len: int = 0, d_icrc: int = 0,

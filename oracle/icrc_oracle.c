@@ -295,6 +295,90 @@ uint16_t oracle_ipv4_checksum(const uint8_t *h) {
 }
 
 /* ---------------------------------------------------------------------------------- */
+/* Receive: is_icrc_valid, then to_rdma_message on buf = pkt[28 .. len-4)              */
+/* ---------------------------------------------------------------------------------- */
+static uint32_t get_be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* Header struct size per opcode: PacketProcessor::to_rdma_message's dispatch
+ * (packet_processor.rs:18-71) over the layouts of packet.rs:286-438. */
+static int rx_header_size(uint8_t opcode) {
+    switch (opcode) {
+    case 0x06: case 0x07: case 0x08: case 0x0A:        /* RdmaWrite{First,Middle,Last,Only}  */
+    case 0x0D: case 0x0E: case 0x0F: case 0x10:        /* RdmaReadResponse*                  */
+        return 28;                                     /* RdmaHeaderReqBthReth               */
+    case 0x09: case 0x0B: return 32;                   /* RdmaHeaderReqBthRethImm            */
+    case 0x0C: return 44;                              /* RdmaHeaderReqBthDoubleReth         */
+    case 0x11: return 16;                              /* RdmaHeaderRespBthAeth              */
+    default: return -1;                                /* Err(PacketError::InvalidOpcode)    */
+    }
+}
+
+int oracle_rx_parse(uint8_t *pkt, uint32_t len, uint64_t off, int zero_trailer, oracle_rx_desc *d) {
+    memset(d, 0, sizeof *d);
+    if (len < 44) {
+        d->icrc_ok = 0xFF;
+        d->status = 3;
+        return ORACLE_OK;
+    }
+    uint8_t saved[4];
+    memcpy(saved, pkt + len - 4, 4);
+    int ok = 0;
+    oracle_is_icrc_valid(pkt, len, &ok); /* zeroes the trailer (packet_processor.rs:350) */
+    if (!zero_trailer) memcpy(pkt + len - 4, saved, 4);
+    d->icrc_ok = ok ? 1 : 0;
+
+    const uint8_t *buf = pkt + 28;             /* UDP payload ... */
+    const uint32_t buf_size = len - 4 - 28;    /* ... with the ICRC stripped */
+    const uint8_t opcode = buf[0] & 0x1F;      /* BTH::get_opcode (packet.rs:61-63) */
+    const uint8_t tran = (buf[0] & 0xE0) >> 5; /* get_transaction_type (57-59) */
+    const int hs = rx_header_size(opcode);
+    if (hs < 0) {
+        d->status = 1;
+        return ORACLE_OK;
+    }
+    if (tran > 6) { /* ToHostWorkRbDescTransType::try_from (types.rs:244-245) */
+        d->status = 2;
+        return ORACLE_OK;
+    }
+    const uint8_t pad = (buf[1] & 0x60) >> 5; /* get_pad_cnt (69-71) */
+    if (buf_size < (uint32_t)hs + pad) {      /* the reference would read past the buffer */
+        d->status = 3;
+        return ORACLE_OK;
+    }
+    d->opcode = opcode;
+    d->tran_type = tran;
+    d->pad_cnt = pad;
+    d->flags = (uint8_t)(((buf[1] & 0x80) ? 0x01 : 0) | ((buf[8] & 0x80) ? 0x02 : 0));
+    d->pkey = (uint16_t)((buf[2] << 8) | buf[3]);   /* get_pkey (79-81) */
+    d->dqpn = get_be32(buf + 4) & 0x00FFFFFFu;       /* get_destination_qpn (83-90) */
+    d->psn = get_be32(buf + 8) & 0x00FFFFFFu;        /* get_psn (96-98); get_ack_req (92-94) */
+    d->payload_offset = off + 28 + (uint64_t)hs;     /* get_data_ptr (267-269) */
+    d->payload_len = buf_size - (uint32_t)hs - pad;  /* get_packet_real_length (74-77) */
+    if (opcode == 0x11) {                            /* AethHeader::new_from_packet (types.rs:318-329) */
+        d->flags |= 0x10;
+        d->aeth_code = (buf[12] & 0x60) >> 5;
+        d->aeth_value = buf[12] & 0x1F;
+        d->aeth_msn = get_be32(buf + 12) & 0x00FFFFFFu;
+        return ORACLE_OK;
+    }
+    d->reth_va = ((uint64_t)get_be32(buf + 12) << 32) | get_be32(buf + 16); /* RETH getters (173-183) */
+    d->reth_rkey = get_be32(buf + 20);
+    d->reth_len = get_be32(buf + 24);
+    if (hs == 32) {
+        d->flags |= 0x04;
+        d->imm = get_be32(buf + 28); /* Immediate::get (packet.rs:249-251) */
+    } else if (hs == 44) {
+        d->flags |= 0x08;
+        d->sec_va = ((uint64_t)get_be32(buf + 28) << 32) | get_be32(buf + 32);
+        d->sec_rkey = get_be32(buf + 36);
+        d->sec_len = get_be32(buf + 40);
+    }
+    return ORACLE_OK;
+}
+
+/* ---------------------------------------------------------------------------------- */
 /* Synthetic workloads                                                                 */
 /* ---------------------------------------------------------------------------------- */
 /* splitmix64 output function (Steele/Lea/Flood 2014) applied to x + golden gamma. */

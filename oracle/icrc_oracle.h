@@ -106,6 +106,19 @@ uint32_t oracle_generate_segments(uint64_t va, uint32_t len, uint32_t path_mtu, 
 /* responser.rs:321-338 (IPv4 header checksum, §8f row 4). */
 uint16_t oracle_ipv4_checksum(const uint8_t *hdr20);
 
+/* --- Receive: is_icrc_valid + to_rdma_message on the stripped UDP payload (§8f row 2) --- */
+/* Same field layout as the product's icrc_rx_desc (include/icrc.h), declared independently. */
+typedef struct oracle_rx_desc {
+    uint64_t reth_va, sec_va, payload_offset;
+    uint32_t payload_len, reth_rkey, reth_len, sec_rkey, sec_len, imm, dqpn, psn, aeth_msn;
+    uint16_t pkey;
+    uint8_t opcode, tran_type, flags, pad_cnt, aeth_code, aeth_value, icrc_ok, status;
+    uint8_t _pad[2];
+} oracle_rx_desc;
+/* pkt = the IPv4 packet at byte offset `off` of the caller's buffer; zero_trailer as
+ * is_icrc_valid.  Fills *d; returns 0. */
+int oracle_rx_parse(uint8_t *pkt, uint32_t len, uint64_t off, int zero_trailer, oracle_rx_desc *d);
+
 /* --- Synthetic workloads ----------------------------------------------- */
 uint64_t oracle_mix64(uint64_t x);
 /* Emulator WRITE send path (write.rs:31-96 + common.rs:73-132 + util.rs:172-186):

@@ -114,6 +114,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_mix64.restype = ctypes.c_uint64
         L.oracle_header_len.argtypes = [ctypes.c_uint8]
         L.oracle_header_len.restype = ctypes.c_int
+        L.oracle_rx_parse.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, u8p]
+        L.oracle_rx_parse.restype = ctypes.c_int
         L.oracle_synth_write.argtypes = [
             u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -240,6 +242,32 @@ def synth_write(total_len: int, pmtu: int, *, local_va: int, remote_va: int, rke
         raise ValueError(f"synth_write: rc={got}")
     off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
     return buf, off, lens
+
+
+RX_DESC_DTYPE = np.dtype([  # oracle_rx_desc (icrc_oracle.h)
+    ("reth_va", "<u8"), ("sec_va", "<u8"), ("payload_offset", "<u8"), ("payload_len", "<u4"),
+    ("reth_rkey", "<u4"), ("reth_len", "<u4"), ("sec_rkey", "<u4"), ("sec_len", "<u4"),
+    ("imm", "<u4"), ("dqpn", "<u4"), ("psn", "<u4"), ("aeth_msn", "<u4"), ("pkey", "<u2"),
+    ("opcode", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("pad_cnt", "u1"),
+    ("aeth_code", "u1"), ("aeth_value", "u1"), ("icrc_ok", "u1"), ("status", "u1"),
+    ("_pad", "u1", (2,)),
+])
+assert RX_DESC_DTYPE.itemsize == 72
+
+
+def rx_parse(base: np.ndarray, off, lens, zero_trailer: bool = False) -> np.ndarray:
+    """is_icrc_valid + to_rdma_message(pkt[28 .. L-4)) per packet (icrc_oracle.c
+    oracle_rx_parse); `base` is modified only when zero_trailer."""
+    off = np.asarray(off, np.uint64)
+    lens = np.asarray(lens, np.uint32)
+    out = np.zeros(off.size, dtype=RX_DESC_DTYPE)
+    for i in range(off.size):
+        o, L = int(off[i]), int(lens[i])
+        if L < 44:
+            out[i]["icrc_ok"], out[i]["status"] = 0xFF, 3
+            continue
+        lib().oracle_rx_parse(_ptr(base) + o, L, o, 1 if zero_trailer else 0, out[i:i + 1].ctypes.data)
+    return out
 
 
 _SEND_OPCODES = {  # (only, first, middle, last): write.rs:31-96, read_response.rs:30-95

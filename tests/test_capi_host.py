@@ -11,6 +11,7 @@ import pytest
 
 import oracle
 import kernel_emu
+import rx_cases
 from golden_kats import KATS
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -27,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 27, names
+    assert len(names) == 28, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -245,3 +246,28 @@ def test_packetizer_header_formulas_match_oracle():
             pkt = wire[o: o + L]
             assert np.all(pkt[56 + ln: L - 4] == 0)
             assert oracle.compute_icrc(pkt) == icrcs[k]
+
+
+def test_rx_desc_layouts_agree():
+    import icrc_amd
+
+    assert icrc_amd.RX_DESC_DTYPE == oracle.RX_DESC_DTYPE
+    assert icrc_amd.WRITE_MSG_DTYPE.itemsize == 88
+
+
+def test_rx_parse_oracle_matches_kernel_model():
+    """The oracle's restatement of to_rdma_message and the kernel's word-level parse agree on
+    every opcode, every pad, and the corrupted cases (icrc_ok excluded: kernel model has no CRC)."""
+    rng = np.random.default_rng(4)
+    pkts = rx_cases.make_packets(rng)
+    off = np.cumsum([0] + [p.size for p in pkts[:-1]]).astype(np.uint64)
+    buf = np.concatenate(pkts)
+    want = oracle.rx_parse(buf, off, [p.size for p in pkts])
+    assert set(want["status"].tolist()) == {0, 1, 2, 3}
+    assert int(np.sum(want["icrc_ok"] == 0)) >= 1
+    for i, p in enumerate(pkts):
+        got = rx_cases.emulate(p, int(off[i]))
+        for f in oracle.RX_DESC_DTYPE.names:
+            if f in ("icrc_ok", "_pad"):
+                continue
+            assert np.all(got[f] == want[i][f]), (i, f, got[f], want[i][f])
