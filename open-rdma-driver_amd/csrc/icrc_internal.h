@@ -39,8 +39,8 @@ struct BatchParams {
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
 };
 
-constexpr int kDefaultVariant = 1;
-constexpr int kMaxVariant = 12;
+constexpr int kDefaultVariant = 13;  // S=1, D=1, nt row loads (A/B: profiles/r01_ab_nt.json)
+constexpr int kMaxVariant = 18;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

@@ -340,9 +340,15 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 
 // Loads of one packet's rows; rows past the
 // packet and every row of a non-regular slot read 0 through the descriptor's range check.
+// ABL = mode | (cache policy << 2): mode 0 real, 1 loads only, 2 CRC only; policy = the aux
+// operand of the row loads (0 default, 2 nt: read-once stream).
+constexpr int abl_mode(int abl) { return abl & 3; }
+constexpr int kStreamAux = 2;  // nt: packets are read once (MI355X_MICROARCH.md nt-weights); +7 % on C1
+constexpr int abl_aux(int abl) { return abl >> 2; }
+
 template <int ABL>
 __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[kRows]) {
-    if constexpr (ABL == 2) {
+    if constexpr (abl_mode(ABL) == 2) {
 #pragma unroll
         for (int j = 0; j < kRows; ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
         return;
@@ -355,7 +361,7 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
     // current packet into vmcnt(0) and drains the prefetch of the next one.
 #pragma unroll
     for (int j = 0; j < kRows; ++j)
-        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, 0);
+        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, abl_aux(ABL));
 }
 
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
@@ -386,7 +392,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                 if (j < rmax) {
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        if constexpr (ABL == 1) acc[s] ^= u[s][j];
+                        if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
                         else acc[s] = step_m64(lds, acc[s], u[s][j], c);
                     }
                 }
@@ -398,7 +404,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                 if (j < rmax) {
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        if constexpr (ABL == 1) {
+                        if constexpr (abl_mode(ABL) == 1) {
                             acc[s] ^= u[s][j];
                         } else {
                             const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
@@ -698,7 +704,7 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
         const int nrec = lc.R > 0 ? static_cast<int>(lc.L - 4u) : 0;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(lc.pkt, 0, nrec, 0x00020000);
         const uint32_t voff = 4u * static_cast<uint32_t>(lc.k0 - 1 + static_cast<int>(lane)) + 256u * static_cast<uint32_t>(lc.j);
-        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, 0);
+        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, kStreamAux);
         if (lc.R > 0) {
             lc.j += 1;
             if (lc.j == lc.R) next_packet(lc, true);
@@ -1082,7 +1088,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
             const_cast<uint8_t *>(src) + (lc.g.R > 0 ? lc.g.src : 0), 0, nrec, 0x00020000);
         // payload byte offset of this lane's word: 4 * pw - 56 (negative -> out of range -> 0)
         const uint32_t voff = 4u * static_cast<uint32_t>(lc.g.k0 - 1 + static_cast<int>(lane) + 64 * lc.j) - 56u;
-        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, 0);
+        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, kStreamAux);
         if (lc.g.R > 0) {
             lc.j += 1;
             if (lc.j == lc.g.R) advance(lc);
@@ -1256,6 +1262,12 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 10: ICRC_LAUNCH(-16, 0, 0); break;  // row stream, 16 rows in flight per wave
     case 11: ICRC_LAUNCH(-24, 0, 0); break;  // row stream, 24 rows
     case 12: ICRC_LAUNCH(-32, 0, 0); break;  // row stream, 32 rows
+    case 13: ICRC_LAUNCH(1, 1, 2 << 2); break;      // variant 1, nt row loads
+    case 14: ICRC_LAUNCH(1, 2, 2 << 2); break;      // variant 3, nt row loads
+    case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2)); break;  // diagnostic: loads only, nt
+    case 16: ICRC_LAUNCH(2, 1, 2 << 2); break;      // variant 2, nt row loads
+    case 17: ICRC_LAUNCH(1, 3, 2 << 2); break;      // variant 4, nt row loads
+    case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2)); break;  // diagnostic: CRC only (same code shape as 15)
     default: ICRC_LAUNCH(1, 2, 0); break;
     }
 }

@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 16, 17])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
