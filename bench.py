@@ -236,7 +236,9 @@ def extra_measurements(eng, stream, args, world):
     ex["roundtrip_16MiB_c3"] = {"packets": w3.n, "ms_per_roundtrip": round(kms, 4),
                                 "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1),
                                 "all_ok": bool((d_ok == 1).all().item())}
-    del d_buf
+    del d_buf, d_off, d_len, d_out, d_ok
+
+    ex.update(fused_send_receive(eng, stream, args, world))
 
     # host-resident: packets in pinned host memory -> H2D -> kernel -> D2H of ICRCs
     nh = min(args.packets, 1 << 18)
@@ -262,6 +264,71 @@ def extra_measurements(eng, stream, args, world):
                     "overlapping copy and kernel) -> ICRCs back to host; PCIe Gen5 x16 bound"}
     ex["host_resident_results_match_device"] = bool(np.array_equal(got, host_icrc_ref(eng, h_np, wh, stream)))
     return ex
+
+
+def fused_send_receive(eng, stream, args, world):
+    """§8f rows 1-3 at C1 scale: the fused send packetizer turning 256 x 16 MiB RDMA WRITE
+    messages (1 Mi x 4156-B packets) into wire packets with trailers, then the fused receive
+    (verify + strip + parse) over the same wire buffer.  Algorithmic HBM bytes per packet:
+    send = 4096 payload read + 4156 wire write + 8 result; receive = 4156 read + 72 descriptor
+    + 1 ok byte written."""
+    import icrc_amd
+
+    out = {}
+    nmsg, msg_bytes, pmtu = max(1, min(args.packets, 3 << 18) // 4096), 16 << 20, 4096  # 3 GiB of payload
+    specs = [dict(local_va=0x7F0000000000 + i * msg_bytes, remote_va=0x7E0000000000 + i * msg_bytes,
+                  payload_offset=i * msg_bytes, total_len=msg_bytes, pmtu=pmtu, rkey=0x2000003, dqpn=2 + i,
+                  psn=0, msn=i & 0xFFFF, dst_ip=0xC0A80003, kind=0) for i in range(nmsg)]
+    msgs = icrc_amd.write_messages(specs, slot_stride=28 + 28 + pmtu + 4)
+    npk = int(msgs["npackets"].sum())
+    src_bytes = nmsg * msg_bytes
+    wire_bytes = npk * (28 + 28 + pmtu + 4)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    d_src = torch.empty(src_bytes, dtype=torch.uint8, device="cuda")
+    for c0 in range(0, src_bytes, 1 << 30):  # < 2^31 elements per torch kernel
+        c1 = min(src_bytes, c0 + (1 << 30))
+        d_src[c0:c1] = torch.randint(0, 256, (c1 - c0,), dtype=torch.uint8, device="cuda", generator=g)
+    torch.cuda.synchronize()
+    d_msgs = dev(msgs.view(np.uint8))
+    d_wire = torch.empty(wire_bytes, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(npk, dtype=torch.int32, device="cuda")
+    d_icrc = torch.zeros(npk, dtype=torch.int32, device="cuda")
+
+    def send():
+        eng.packetize(d_src.data_ptr(), src_bytes, d_msgs.data_ptr(), nmsg, npk, d_wire.data_ptr(), wire_bytes,
+                      d_len.data_ptr(), d_icrc.data_ptr(), stream)
+
+    _, kms = time_kernel(send, args.steps, args.warmup, world)
+    torch.cuda.synchronize()
+    lens_ok = bool((d_len == 28 + 28 + pmtu + 4).all().item())
+    log(f"packetize: {npk} packets, {kms:.4f} ms, lengths ok {lens_ok}")
+    alg = npk * (4096 + 4156 + 8)
+    out["packetize_send"] = {"packets": npk, "kernel_ms": round(kms, 4),
+                             "wire_GiB/s": round(wire_bytes / (kms * 1e-3) / GIB, 1),
+                             "hbm_GB/s": round(alg / (kms * 1e-3) / 1e9, 1),
+                             "frac_of_peak": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "lengths_ok": lens_ok}
+    if not lens_ok:
+        return out
+    del d_src
+    d_off = torch.arange(npk, dtype=torch.int64, device="cuda") * (28 + 28 + pmtu + 4)
+    d_desc = torch.empty(npk * icrc_amd.RX_DESC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    d_ok = torch.zeros(npk, dtype=torch.uint8, device="cuda")
+
+    def recv():
+        eng.rx_parse(d_wire.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), npk, d_desc.data_ptr(), d_ok.data_ptr(),
+                     stream=stream)
+
+    _, kms = time_kernel(recv, args.steps, args.warmup, world)
+    alg = npk * (4156 + 72 + 1)
+    desc = d_desc[: 64 * 72].cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+    out["rx_verify_parse"] = {"packets": npk, "kernel_ms": round(kms, 4),
+                              "GiB/s": round(wire_bytes / (kms * 1e-3) / GIB, 1),
+                              "hbm_GB/s": round(alg / (kms * 1e-3) / 1e9, 1),
+                              "frac_of_peak": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "all_ok": bool((d_ok == 1).all().item()),
+                              "payload_len_ok": bool(np.all(desc["payload_len"] == pmtu))}
+    return out
 
 
 def host_icrc_ref(eng, h_np, wh, stream):

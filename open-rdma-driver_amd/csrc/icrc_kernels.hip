@@ -51,13 +51,18 @@ constexpr uint32_t kSel1 = 0x0C0C0501u;  // [slot+128, s.b1, 0,  0]
 constexpr uint32_t kSel2 = 0x0C020600u;  // [slot,   s.b2, 0x01, 0]
 constexpr uint32_t kSel3 = 0x0C020701u;  // [slot+128, s.b3, 0x01, 0]
 
-// M^64(s) ^ u: four byte lookups; u is folded in before the last read arrives.
+// Three-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// M^64(s) ^ u: four byte lookups; u is folded in with the first two reads (two v_bitop3).
 __device__ __forceinline__ uint32_t step_m64(const char *lds, uint32_t s, uint32_t u, const LaneConsts &c) {
     const uint32_t r0 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel0));
     const uint32_t r1 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel1));
     const uint32_t r2 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel2));
     const uint32_t r3 = lds_at(lds, __builtin_amdgcn_perm(s, c.pc, kSel3));
-    return ((r0 ^ r1) ^ (r2 ^ u)) ^ r3;
+    return xor3(xor3(u, r0, r1), r2, r3);
 }
 
 __device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const LaneConsts &c) {
@@ -69,7 +74,7 @@ __device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uin
     uint32_t r[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, fin + n * 4096u + (((acc >> (4 * n)) & 15u) << 8));
-    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
 // XOR over the 64 lanes with DPP (VALU, no LDS round trips): two quad permutes and two
@@ -353,6 +358,7 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
         for (int j = 0; j < kRows; ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
         return;
     }
+    constexpr int kAux = abl_aux(ABL);
     const int nrec = m.kind == 1 ? static_cast<int>(m.L - 4u) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
     const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
@@ -361,7 +367,7 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
     // current packet into vmcnt(0) and drains the prefetch of the next one.
 #pragma unroll
     for (int j = 0; j < kRows; ++j)
-        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, abl_aux(ABL));
+        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, kAux);
 }
 
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
@@ -386,7 +392,16 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             u[s][1] |= head_mask(k + 64);
         }
         // One straight-line block per row for all S chains (the scheduler interleaves them).
-        if (same) {
+        if (same && rmax == kRows) {  // full-MTU packets (4 KiB): no per-row guard branches
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                    else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                }
+            }
+        } else if (same) {
 #pragma unroll
             for (int j = 1; j < kRows; ++j) {
                 if (j < rmax) {
