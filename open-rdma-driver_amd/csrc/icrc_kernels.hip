@@ -552,69 +552,65 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) <<
 // stores dword k of the 72-byte icrc_rx_desc.
 __device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t hdr, uint64_t off, uint32_t L,
                                          uint32_t icrc_ok, uint32_t lane) {
-    uint32_t f[18];
-#pragma unroll
-    for (int k = 0; k < 18; ++k) f[k] = 0u;
-    uint32_t status = ICRC_RX_TRUNCATED;
-    if (L >= ICRC_MIN_PACKET) {
-        const uint32_t w7 = __builtin_amdgcn_readlane(hdr, 7);
-        const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
-        // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
-        const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
-                          : (op == 0x0Cu)                 ? 44u
-                          : (op == 0x11u)                 ? 16u
-                          : (op >= 0x06u && op <= 0x10u)  ? 28u
-                                                          : 0u;
-        if (hs == 0u) {
-            status = ICRC_RX_INVALID_OPCODE;
-        } else if (tran > 6u) {
-            status = ICRC_RX_INVALID_TRANS_TYPE;
-        } else if (L - 32u < hs + pad) {  // buf_size = L - 28 - 4
-            status = ICRC_RX_TRUNCATED;
-        } else {
-            status = ICRC_RX_OK;
-            const uint32_t w8 = __builtin_amdgcn_readlane(hdr, 8), w9 = __builtin_amdgcn_readlane(hdr, 9);
-            const uint32_t w10 = __builtin_amdgcn_readlane(hdr, 10);
-            uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u);
-            const uint64_t poff = off + 28u + hs;
-            f[4] = static_cast<uint32_t>(poff);
-            f[5] = static_cast<uint32_t>(poff >> 32);
-            f[6] = L - 32u - hs - pad;
-            f[12] = bswap32(w8) & 0xFFFFFFu;
-            f[13] = bswap32(w9) & 0xFFFFFFu;
-            uint32_t code = 0, value = 0;
-            if (hs == 16u) {
-                flags |= ICRC_RX_ACKNOWLEDGE;
-                code = (w10 >> 5) & 3u;
-                value = w10 & 0x1Fu;
-                f[14] = bswap32(w10) & 0xFFFFFFu;
-            } else {
-                const uint32_t w11 = __builtin_amdgcn_readlane(hdr, 11), w12 = __builtin_amdgcn_readlane(hdr, 12);
-                const uint32_t w13 = __builtin_amdgcn_readlane(hdr, 13);
-                f[0] = bswap32(w11);
-                f[1] = bswap32(w10);
-                f[7] = bswap32(w12);
-                f[8] = bswap32(w13);
-                const uint32_t w14 = __builtin_amdgcn_readlane(hdr, 14);
-                if (hs == 32u) {
-                    flags |= ICRC_RX_HAS_IMM;
-                    f[11] = bswap32(w14);
-                } else if (hs == 44u) {
-                    flags |= ICRC_RX_HAS_SECONDARY_RETH;
-                    f[2] = bswap32(__builtin_amdgcn_readlane(hdr, 15));
-                    f[3] = bswap32(w14);
-                    f[9] = bswap32(__builtin_amdgcn_readlane(hdr, 16));
-                    f[10] = bswap32(__builtin_amdgcn_readlane(hdr, 17));
-                }
-            }
-            f[15] = bswap16(w7 >> 16) | (op << 16) | (tran << 24);
-            f[16] = flags | (pad << 8) | (code << 16) | (value << 24);
-        }
-    }
-    f[17] = (icrc_ok & 0xFFu) | (status << 8);
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 18; ++k) v = (lane == static_cast<uint32_t>(k)) ? f[k] : v;
+    // Wave-uniform part: BTH byte 0/1 and the header size decide the packet's shape.
+    const uint32_t w7 = __builtin_amdgcn_readlane(hdr, 7);
+    const uint32_t w9 = __builtin_amdgcn_readlane(hdr, 9);
+    const uint32_t w10 = __builtin_amdgcn_readlane(hdr, 10);
+    const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+    // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
+    const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                      : (op == 0x0Cu)                 ? 44u
+                      : (op == 0x11u)                 ? 16u
+                      : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                      : 0u;
+    uint32_t status;
+    if (L < ICRC_MIN_PACKET) status = ICRC_RX_TRUNCATED;
+    else if (hs == 0u) status = ICRC_RX_INVALID_OPCODE;
+    else if (tran > 6u) status = ICRC_RX_INVALID_TRANS_TYPE;
+    else if (L - 32u < hs + pad) status = ICRC_RX_TRUNCATED;  // buf_size = L - 28 - 4
+    else status = ICRC_RX_OK;
+    const bool ack = hs == 16u;
+    uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                     (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                     (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+    const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+    const uint64_t poff = off + 28u + hs;
+
+    // Per-lane part: dword `lane` of icrc_rx_desc.  Big-endian header fields are gathered from
+    // the header word that holds them (one ds_bpermute) and byte-swapped (one v_perm).
+    //   dword: 0 va.lo  1 va.hi  2 sec.lo  3 sec.hi  7 rkey  8 dlen  9 sec rkey  10 sec dlen
+    //          11 imm  12 dqpn  13 psn  14 aeth msn          <- header words 11 10 15 14 12 13
+    //                                                           16 17 14 8 9 10
+    uint32_t src = 0;
+    src = lane == 0u ? 11u : src;
+    src = lane == 1u ? 10u : src;
+    src = lane == 2u ? 15u : src;
+    src = lane == 3u ? 14u : src;
+    src = lane == 7u ? 12u : src;
+    src = lane == 8u ? 13u : src;
+    src = lane == 9u ? 16u : src;
+    src = lane == 10u ? 17u : src;
+    src = lane == 11u ? 14u : src;
+    src = lane == 12u ? 8u : src;
+    src = lane == 13u ? 9u : src;
+    src = lane == 14u ? 10u : src;
+    const uint32_t g = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src << 2), static_cast<int>(hdr)));
+    uint32_t v = __builtin_amdgcn_perm(g, g, 0x00010203u);  // bswap32
+    const bool reth = !ack;                                  // General metadata: RETH present
+    bool keep = (lane <= 1u || lane == 7u || lane == 8u) ? reth
+              : (lane == 2u || lane == 3u || lane == 9u || lane == 10u) ? hs == 44u
+              : (lane == 11u) ? hs == 32u
+              : (lane == 14u) ? ack
+              : (lane == 12u || lane == 13u);
+    v = keep ? v : 0u;
+    v = (lane >= 12u && lane <= 14u) ? (v & 0xFFFFFFu) : v;
+    v = lane == 4u ? static_cast<uint32_t>(poff) : v;
+    v = lane == 5u ? static_cast<uint32_t>(poff >> 32) : v;
+    v = lane == 6u ? L - 32u - hs - pad : v;
+    v = lane == 15u ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : v;
+    v = lane == 16u ? (flags | (pad << 8) | (code << 16) | (value << 24)) : v;
+    v = status != ICRC_RX_OK ? 0u : v;  // on error every parsed field is 0
+    v = lane == 17u ? ((icrc_ok & 0xFFu) | (status << 8)) : v;
     if (lane < 18u) reinterpret_cast<uint32_t *>(rx + i)[lane] = v;
 }
 

@@ -38,6 +38,16 @@ def main():
 
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * L
     d_len = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    eng.set_variant(10)  # row stream, ragged meta blocks: compute, then verify
+    d_out2 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out2.data_ptr(), False, 0, s)
+    torch.cuda.synchronize()
+    say(f"stage 3a row-stream compute ragged ok: same={bool(torch.equal(d_out, d_out2))}")
+    d_ok.zero_()
+    eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), False, 0, s)
+    torch.cuda.synchronize()
+    say(f"stage 3b row-stream verify ragged ok: all_ok={bool((d_ok == 1).all().item())}")
+    eng.set_variant(-1)
     d_ok.zero_()
     eng.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(), d_ok.data_ptr(), stream=s)
     torch.cuda.synchronize()
