@@ -160,6 +160,16 @@ int icrc_rx_parse_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d
                          icrc_rx_desc *d_desc, uint8_t *d_ok, int zero_trailer, uint32_t *d_nerr,
                          void *stream);
 
+/* ---- batched IPv4 header checksum (§8f row 4) ----------------------------------------------
+ * calculate_ipv4_checksum (rust_driver/src/responser.rs:321-338): the one's-complement sum of
+ * the ten big-endian 16-bit words of the 20-byte IPv4 header at d_base + off (d_off NULL =>
+ * i * stride), complemented.  fill == 0: over the header as stored (a header carrying a valid
+ * checksum gives 0); fill != 0: with bytes 10-11 taken as 0 and the result then stored there
+ * big-endian (responser.rs:198-201).  d_csum (may be NULL) receives the u16 per packet.  The
+ * ICRC masks bytes 10-11, so filling never changes a packet's ICRC. */
+int icrc_ipv4_checksum_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d_off,
+                              uint64_t stride, uint32_t n, uint16_t *d_csum, int fill, void *stream);
+
 /* ---- packet synthesis on the device (bench inputs; precursor of the fused packetizer) --- */
 /* Packet i = header template d_hdr[hdr_index*64 .. +hdr_len) ‖ payload ‖ zero pad ‖ zero
  * ICRC slot, written at d_base + offset.  Payload byte q = byte ((pos+q) & 7) of
@@ -209,9 +219,19 @@ typedef struct icrc_write_msg {
     uint16_t ip_id;          /* generate_payload_from_msg uses 1 (net/util.rs:179) */
     uint8_t kind;            /* 0 = RDMA WRITE, 1 = RDMA READ RESPONSE */
     uint8_t tran_type;       /* RC = 0 */
-    uint8_t _pad[6];
+    uint8_t flags;           /* ICRC_WRITE_* below */
+    uint8_t _pad[5];
 } icrc_write_msg; /* 88 bytes */
-/* Number of packets generate_segments_from_request yields (common.rs:152-176); 0 if pmtu == 0. */
+/* Fill the IPv4 header checksum (RFC 791, as smoltcp's fill_checksum does when the emulator
+ * builds the frame, net_agent.rs:93; calculate_ipv4_checksum, responser.rs:321-338).  The
+ * ICRC masks those bytes, so it is the same either way.  Default: 0, as PacketWriter leaves it. */
+#define ICRC_WRITE_FILL_IPV4_CSUM 0x01u
+/* Segment on the remote VA (rust_driver: calculate_packet_cnt / get_first_packet_max_length,
+ * rust_driver/src/utils.rs:19-33) instead of the local VA (emulator, common.rs:152-176). */
+#define ICRC_WRITE_SEG_BY_REMOTE_VA 0x02u
+/* Number of packets generate_segments_from_request yields (common.rs:152-176) for a message
+ * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_SEG_BY_REMOTE_VA);
+ * 0 if pmtu == 0. */
 uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu);
 /* Wire length of segment s (IPv4 + UDP + BTH + RETH + payload + pad + ICRC). */
 uint32_t icrc_write_packet_len(uint64_t local_va, uint32_t total_len, uint32_t pmtu, uint32_t s);

@@ -519,6 +519,15 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     return icrc::launch_rx(p, grid_for(e, n), stream);
 }
 
+int icrc_ipv4_checksum_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off, uint64_t stride, uint32_t n,
+                              uint16_t *d_csum, int fill, void *stream) {
+    if (!e || !d_base) return ICRC_EINVAL;
+    if (n == 0) return ICRC_OK;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    return icrc::launch_ipv4_checksum(d_base, d_off, stride, n, d_csum, fill ? 1 : 0, stream);
+}
+
 uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {
     if (pmtu == 0) return 0;
     const uint32_t first = icrc::write_first_segment(local_va, total_len, pmtu);

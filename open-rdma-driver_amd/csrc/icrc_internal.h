@@ -65,6 +65,8 @@ struct PacketizeParams {
     const uint32_t *table;
 };
 int launch_packetize(const PacketizeParams &p, int grid, void *stream);
+int launch_ipv4_checksum(uint8_t *base, const uint64_t *off, uint64_t stride, uint32_t n, uint16_t *csum, int fill,
+                         void *stream);
 
 // Segmentation shared by host and tests (generate_segments_from_request, common.rs:152-176).
 inline uint32_t write_first_segment(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {

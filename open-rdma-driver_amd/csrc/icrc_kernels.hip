@@ -907,7 +907,8 @@ __device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t n
 
 __device__ __forceinline__ void seg_info(const MsgRegs &m, uint32_t s, SegInfo &g) {
     const uint32_t total = msg_u32(m, kMTotal), pmtu = msg_u32(m, kMPmtu);
-    const uint32_t lva = static_cast<uint32_t>(msg_u64(m, kMLocalVa));
+    const bool by_remote = ((msg_u32(m, kMKind) >> 16) & ICRC_WRITE_SEG_BY_REMOTE_VA) != 0u;
+    const uint32_t lva = static_cast<uint32_t>(msg_u64(m, by_remote ? kMRemoteVa : kMLocalVa));
     uint32_t first = pmtu - lva % pmtu;
     first = total < first ? total : first;
     if (s == 0) {
@@ -955,6 +956,15 @@ __device__ __forceinline__ void build_header(const MsgRegs &m, uint32_t s, const
     h.w[11] = bswap32(static_cast<uint32_t>(va));
     h.w[12] = bswap32(msg_u32(m, kMRkey));
     h.w[13] = bswap32(msg_u32(m, kMRethLen));
+    if ((msg_u32(m, kMKind) >> 16) & ICRC_WRITE_FILL_IPV4_CSUM) {
+        // RFC 791 one's-complement sum of the ten big-endian 16-bit header words
+        const uint32_t src = msg_u32(m, kMSrcIp), dst = msg_u32(m, kMDstIp);
+        uint32_t sum = 0x4500u + (g.L & 0xFFFFu) + ipid + 0x4011u + (src >> 16) + (src & 0xFFFFu) + (dst >> 16) +
+                       (dst & 0xFFFFu);
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+        sum = (sum & 0xFFFFu) + (sum >> 16);
+        h.w[2] |= bswap16(~sum & 0xFFFFu) << 16;
+    }
 }
 
 __device__ __forceinline__ uint32_t header_word(const PacketHdr &h, int pw) {
@@ -1201,6 +1211,28 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     }
 }
 
+// ---- batched IPv4 header checksum (responser.rs:321-338) ---------------------------------------
+// One thread per packet: 20 header bytes, ten big-endian words, end-around carry, complement.
+__global__ __launch_bounds__(256) void icrc_ipv4_checksum_kernel(uint8_t *base, const uint64_t *off, uint64_t stride,
+                                                                 uint32_t n, uint16_t *csum, int fill) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    uint8_t *h = base + (off ? off[i] : static_cast<uint64_t>(i) * stride);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 20; k += 2) {
+        const uint32_t w = (static_cast<uint32_t>(h[k]) << 8) | h[k + 1];
+        sum += (fill && k == 10) ? 0u : w;
+    }
+    while (sum >> 16) sum = (sum & 0xFFFFu) + (sum >> 16);
+    const uint32_t c = ~sum & 0xFFFFu;
+    if (fill) {
+        h[10] = static_cast<uint8_t>(c >> 8);
+        h[11] = static_cast<uint8_t>(c);
+    }
+    if (csum) csum[i] = static_cast<uint16_t>(c);
+}
+
 // ---- packet synthesis ----------------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -1305,6 +1337,14 @@ int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((icrc_rx_kernel<16>), dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_ipv4_checksum(uint8_t *base, const uint64_t *off, uint64_t stride, uint32_t n, uint16_t *csum, int fill,
+                         void *stream) {
+    if (n == 0) return ICRC_OK;
+    hipLaunchKernelGGL(icrc_ipv4_checksum_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), base, off, stride, n, csum, fill);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

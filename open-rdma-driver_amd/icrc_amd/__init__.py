@@ -94,8 +94,9 @@ WRITE_MSG_DTYPE = np.dtype([
     ("total_len", "<u4"), ("reth_len", "<u4"), ("pmtu", "<u4"), ("rkey", "<u4"), ("dqpn", "<u4"),
     ("psn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("first_packet", "<u4"),
     ("npackets", "<u4"), ("slot_stride", "<u4"), ("msn", "<u2"), ("ip_id", "<u2"),
-    ("kind", "u1"), ("tran_type", "u1"), ("_pad", "u1", (6,)),
+    ("kind", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("_pad", "u1", (5,)),
 ])
+WRITE_FILL_IPV4_CSUM, WRITE_SEG_BY_REMOTE_VA = 0x01, 0x02
 assert WRITE_MSG_DTYPE.itemsize == 88
 MSG_WRITE, MSG_READ_RESPONSE = 0, 1
 
@@ -153,6 +154,7 @@ def _load() -> ctypes.CDLL:
         "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
         "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
         "icrc_rx_parse_device": (i32, [vp, vp, vp, vp, u64, u32, u32, vp, vp, i32, vp, vp]),
+        "icrc_ipv4_checksum_device": (i32, [vp, vp, vp, u64, u32, vp, i32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -383,6 +385,12 @@ class Engine:
                                         d_desc, d_ok or None, 1 if zero_trailer else 0, d_nerr or None,
                                         stream or None), "icrc_rx_parse_device")
 
+    def ipv4_checksum(self, d_base: int, n: int, d_off: int = 0, stride: int = 0, d_csum: int = 0,
+                      fill: bool = False, stream: Optional[int] = None) -> None:
+        """Batched IPv4 header checksum (icrc_ipv4_checksum_device, responser.rs:321-338)."""
+        _check(lib.icrc_ipv4_checksum_device(self.handle, d_base, d_off or None, stride, n, d_csum or None,
+                                             1 if fill else 0, stream or None), "icrc_ipv4_checksum_device")
+
     def packetize(self, d_src: int, src_bytes: int, d_msgs: int, nmsgs: int, npackets: int,
                   d_wire: int, wire_bytes: int, d_pkt_len: int = 0, d_icrc: int = 0,
                   stream: Optional[int] = None) -> None:
@@ -419,7 +427,8 @@ def write_messages(specs, slot_stride: int = 0, base_out: int = 0) -> np.ndarray
             m["reth_len"] = s["total_len"]
         if "ip_id" not in s:
             m["ip_id"] = 1  # generate_payload_from_msg (net/util.rs:179)
-        n = write_segment_count(int(s.get("local_va", 0)), int(s["total_len"]), int(s["pmtu"]))
+        seg_va = s.get("remote_va", 0) if int(s.get("flags", 0)) & WRITE_SEG_BY_REMOTE_VA else s.get("local_va", 0)
+        n = write_segment_count(int(seg_va), int(s["total_len"]), int(s["pmtu"]))
         stride = int(s.get("slot_stride", slot_stride or ((int(s["pmtu"]) + 64 + 3) & ~3)))
         m["npackets"], m["first_packet"], m["slot_stride"] = n, first, stride
         if "out_offset" not in s:

@@ -287,7 +287,9 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
     lens = np.zeros(npk, dtype=np.uint32)
     icrcs = np.zeros(npk, dtype=np.uint32)
     for m in msgs:
-        segs = generate_segments(int(m["local_va"]), int(m["total_len"]), int(m["pmtu"]))
+        flags = int(m["flags"]) if "flags" in m.dtype.names else 0
+        seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])  # rust_driver utils.rs:19-33
+        segs = generate_segments(seg_va, int(m["total_len"]), int(m["pmtu"]))
         assert len(segs) == int(m["npackets"])
         only, first, middle, last = _SEND_OPCODES[int(m["kind"])]
         pos = 0
@@ -318,6 +320,9 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
             rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]))
             if rc:
                 raise ValueError(f"packet_write rc={rc}")
+            if flags & 0x01:  # IPv4 checksum filled (responser.rs:198-201 / smoltcp fill_checksum)
+                c = ipv4_checksum(pkt[:20])  # bytes 10-11 are 0 as PacketWriter left them
+                pkt[10], pkt[11] = c >> 8, c & 0xFF
             icrc = int(pkt[-4:].view("<u4")[0])
             o = int(m["out_offset"]) + s * int(m["slot_stride"])
             wire[o: o + pkt.size] = pkt

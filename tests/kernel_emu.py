@@ -70,7 +70,9 @@ def packetizer_header_words(m, s: int) -> tuple:
     """icrc_packetize_kernel's seg_info + build_header for segment s of message m (a
     WRITE_MSG_DTYPE record): returns (14 LE header words, payload len, wire length L)."""
     total, pmtu = int(m["total_len"]), int(m["pmtu"])
-    first = min(total, pmtu - (int(m["local_va"]) & 0xFFFFFFFF) % pmtu)
+    flags = int(m["flags"])
+    seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])
+    first = min(total, pmtu - (seg_va & 0xFFFFFFFF) % pmtu)
     if s == 0:
         start, ln = 0, first
     else:
@@ -102,6 +104,12 @@ def packetizer_header_words(m, s: int) -> tuple:
     w[11] = _bswap32(va & 0xFFFFFFFF)
     w[12] = _bswap32(int(m["rkey"]))
     w[13] = _bswap32(int(m["reth_len"]))
+    if flags & 0x01:
+        src, dst = int(m["src_ip"]), int(m["dst_ip"])
+        sm = 0x4500 + L + int(m["ip_id"]) + 0x4011 + (src >> 16) + (src & 0xFFFF) + (dst >> 16) + (dst & 0xFFFF)
+        sm = (sm & 0xFFFF) + (sm >> 16)
+        sm = (sm & 0xFFFF) + (sm >> 16)
+        w[2] |= _bswap16(~sm & 0xFFFF) << 16
     return tuple(w), ln, L
 
 

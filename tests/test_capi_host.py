@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 28, names
+    assert len(names) == 29, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -222,7 +222,24 @@ def _packetizer_specs(rng):
         dict(local_va=0x3FF, remote_va=0x1234567, payload_offset=20008, total_len=5000, pmtu=1024,
              rkey=0xFFFFFFFF, dqpn=9, psn=0xFFFFFE, msn=0xFFFF, dst_ip=0xC0A80004, kind=1,
              reth_len=123456789),
+        dict(local_va=0x1000, remote_va=0x7F00000000F0, payload_offset=0, total_len=9000, pmtu=4096,
+             rkey=5, dqpn=4, psn=77, msn=3, dst_ip=0xC0A80003, kind=0, flags=0x03, ip_id=0xBEEF),
+        dict(local_va=0x10, remote_va=0x2000, payload_offset=100, total_len=600, pmtu=256, rkey=6,
+             dqpn=5, psn=0, msn=4, dst_ip=0xFFFFFFFF, src_ip=0xFFFFFFFF, kind=1, flags=0x01, ip_id=0xFFFF),
     ]
+
+
+def test_packetizer_flags_change_layout_as_declared():
+    import icrc_amd
+
+    rng = np.random.default_rng(1)
+    msgs = icrc_amd.write_messages(_packetizer_specs(rng))
+    # remote-VA segmentation: 0x7F00000000F0 % 4096 = 0xF0 -> first segment 4096 - 240
+    m = msgs[4]
+    assert m["npackets"] == icrc_amd.write_segment_count(0x7F00000000F0, 9000, 4096) == 3
+    assert icrc_amd.write_segment_count(0x1000, 9000, 4096) == 3
+    _, ln, _ = kernel_emu.packetizer_header_words(m, 0)
+    assert ln == 4096 - 0xF0
 
 
 def test_packetizer_header_formulas_match_oracle():

@@ -351,7 +351,8 @@ def _random_specs(rng, nmsg, aligned=True):
                           payload_offset=off, total_len=ln, pmtu=pmtu, rkey=int(rng.integers(0, 1 << 32)),
                           dqpn=int(rng.integers(0, 1 << 24)), psn=int(rng.integers(0, 1 << 24)),
                           msn=int(rng.integers(0, 1 << 16)), dst_ip=int(rng.integers(0, 1 << 32)),
-                          kind=int(rng.integers(0, 2)), ip_id=int(rng.integers(0, 1 << 16))))
+                          kind=int(rng.integers(0, 2)), ip_id=int(rng.integers(0, 1 << 16)),
+                          flags=int(rng.integers(0, 4))))
         off += ln + int(rng.integers(0, 8))
     return specs, off
 
@@ -549,3 +550,40 @@ def test_send_receive_roundtrip(engine):
     for s in specs:
         a, ln = s["payload_offset"], s["total_len"]
         np.testing.assert_array_equal(mr[a: a + ln], src[a: a + ln])
+
+
+# ---- batched IPv4 header checksum (icrc_ipv4_checksum_device) -------------------------------
+def test_ipv4_checksum_reference_vectors_and_fill(engine):
+    """responser.rs:370-393 vectors (checksum over the stored header), then fill mode on random
+    headers at odd offsets: the stored checksum equals the oracle's and re-summing gives 0."""
+    from golden_kats import IPV4_HEADERS
+
+    rng = np.random.default_rng(12)
+    hdrs = [np.frombuffer(h, np.uint8) for h, _ in IPV4_HEADERS]
+    hdrs += [rng.integers(0, 256, 20, dtype=np.uint8) for _ in range(500)]
+    off = np.cumsum([0] + [21] * (len(hdrs) - 1)).astype(np.uint64)  # odd offsets: byte path
+    buf = np.zeros(int(off[-1]) + 21, np.uint8)
+    for o, h in zip(off, hdrs):
+        buf[int(o): int(o) + 20] = h
+    zeroed = [h.copy() for h in hdrs]
+    for z in zeroed:
+        z[10:12] = 0
+    n = len(hdrs)
+    d_buf, d_off = dev(buf), dev(off)
+    d_c = torch.zeros(n, dtype=torch.int16, device="cuda")
+    engine.ipv4_checksum(d_buf.data_ptr(), n, d_off=d_off.data_ptr(), d_csum=d_c.data_ptr(), stream=stream_handle())
+    torch.cuda.synchronize()
+    raw = d_c.cpu().numpy().view(np.uint16)
+    assert [int(x) for x in raw] == [oracle.ipv4_checksum(h) for h in hdrs]
+    for (h, want), got in zip(IPV4_HEADERS, raw):
+        assert int(got) == want
+    engine.ipv4_checksum(d_buf.data_ptr(), n, d_off=d_off.data_ptr(), d_csum=d_c.data_ptr(), fill=True,
+                         stream=stream_handle())
+    torch.cuda.synchronize()
+    filled = d_buf.cpu().numpy()
+    got = d_c.cpu().numpy().view(np.uint16)
+    for i, (o, z) in enumerate(zip(off, zeroed)):
+        c = oracle.ipv4_checksum(z)
+        assert int(got[i]) == c
+        h = filled[int(o): int(o) + 20]
+        assert (int(h[10]) << 8 | int(h[11])) == c and oracle.ipv4_checksum(h) == 0
