@@ -370,177 +370,6 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
         u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, kAux);
 }
 
-// Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
-// the wave's result buffer.
-template <int MODE, int S, int ABL>
-__device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows],
-                                            uint32_t q0, ResultBuf &rb) {
-    int rmax = 0;
-    bool same = true;  // every slot regular with the same row count (the common case)
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        if (m[s].kind == 1 && m[s].R > rmax) rmax = m[s].R;
-        same = same && m[s].kind == 1 && m[s].R == m[0].R;
-    }
-    if (rmax > 0) {
-        uint32_t acc[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int k = m[s].k0 + static_cast<int>(lane);
-            acc[s] = u[s][0] | head_mask(k);
-            u[s][1] |= head_mask(k + 64);
-        }
-        // One straight-line block per row for all S chains (the scheduler interleaves them).
-        if (same && rmax == kRows) {  // full-MTU packets (4 KiB): no per-row guard branches
-#pragma unroll
-            for (int j = 1; j < kRows; ++j) {
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
-                    else acc[s] = step_m64(lds, acc[s], u[s][j], c);
-                }
-            }
-        } else if (same) {
-#pragma unroll
-            for (int j = 1; j < kRows; ++j) {
-                if (j < rmax) {
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
-                        else acc[s] = step_m64(lds, acc[s], u[s][j], c);
-                    }
-                }
-            }
-        } else {
-            // a chain past its own last row keeps its value through a select
-#pragma unroll
-            for (int j = 1; j < kRows; ++j) {
-                if (j < rmax) {
-#pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        if constexpr (abl_mode(ABL) == 1) {
-                            acc[s] ^= u[s][j];
-                        } else {
-                            const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
-                            acc[s] = (j < m[s].R) ? t : acc[s];
-                        }
-                    }
-                }
-            }
-        }
-        uint32_t fin[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-            if (m[s].kind == 1)
-                rb_put(rb, q0 + s, packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane));
-    }
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-        if (m[s].kind == 2) rb_put(rb, q0 + s, handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane));
-}
-
-// A wave owns the contiguous packet range [lo, lo + nq) and walks it in sets of S packets
-// (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
-// processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
-// ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
-template <int MODE, int S, int D, int ABL>
-__device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                              uint32_t lane, uint32_t lo, uint32_t nq) {
-    constexpr int B = D + 1;
-    static_assert(64 % S == 0, "sets must not straddle a 64-packet result block");
-    if (nq == 0) return;
-    const uint32_t nsets = (nq + S - 1) / S;
-    const bool ragged = p.off != nullptr || p.len != nullptr;
-    MetaBlock mb;
-    mb.block = -1;
-    mb.off_lo = mb.off_hi = mb.len = 0;
-    ResultBuf rb;
-    rb.v = 0;
-    rb.valid = 0;
-    SlotMeta m[B][S];
-    uint32_t u[B][S][kRows];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (static_cast<uint32_t>(d) < nsets) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                slot_meta(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
-                slot_load<ABL>(m[d][s], lane, u[d][s]);
-            }
-        }
-    }
-    for (uint32_t t = 0; t < nsets; t += B) {
-        const bool cont = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
-            constexpr int b = decltype(bc)::value;
-            constexpr int bp = (b + D) % B;
-            const uint32_t ts = t + b;
-            if (ts >= nsets) return false;
-            const uint32_t tp = ts + D;
-            // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor)
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
-                slot_load<ABL>(m[bp][s], lane, u[bp][s]);
-            }
-            const uint32_t q0 = ts * S;
-            process_set<MODE, S, ABL>(p, lds, c, lane, m[b], u[b], q0, rb);
-            const uint32_t qn = q0 + S;  // next unprocessed
-            if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
-            return true;
-        });
-        if (!cont) return;
-    }
-}
-
-// ---- row-stream path ------------------------------------------------------------------------
-// A wave's chunk is one flat sequence of 256-byte rows (the sum of R over its regular packets,
-// in packet order).  A ring of RD row loads stays in flight (RD * 256 B per wave); the
-// process side consumes rows in the same order, restarting the Horner accumulator at each
-// packet's first row and finalising at its last.  A short packet costs only its own rows,
-// a long one needs no special path, and every ring load is unconditional (exact vmcnt
-// accounting).  Misaligned packets and L % 4 != 0 are skipped by the stream and done by a
-// tail loop; L < 44 packets are recorded as errors when the process cursor passes them.
-struct RowCursor {  // wave-uniform
-    uint32_t q;     // packet sequence number within the chunk
-    int j;          // row within the packet
-    int R;          // rows of the current packet (0 = past the end)
-    int k0;
-    uint8_t *pkt;
-    uint32_t L;
-};
-
-// R >= 1: regular packet; 0: L < 44 (error); -1: irregular (generic path).
-__device__ __forceinline__ int classify(const uint8_t *pkt, uint32_t L, int &k0) {
-    if (L < ICRC_MIN_PACKET) return 0;
-    if (((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) != 0) return -1;
-    const int N = 1 + static_cast<int>((L - 4u) >> 2);
-    const int R = (N + 63) >> 6;
-    k0 = N - 64 * R;
-    return R;
-}
-
-__device__ __forceinline__ void meta_read(const MetaBlock &mb, uint32_t q, uint64_t &off, uint32_t &L) {
-    const int l = static_cast<int>(q & 63u);
-    off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
-          (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
-    L = __builtin_amdgcn_readlane(mb.len, l);
-}
-
-// Result buffer keyed by 64-packet block: switching block flushes the previous one.
-template <int MODE>
-__device__ __forceinline__ void rb_record(const BatchParams &p, ResultBuf &rb, int &rb_block, uint32_t lo,
-                                          uint32_t q, uint32_t r, uint32_t lane) {
-    const int blk = static_cast<int>(q >> 6);
-    if (blk != rb_block) {
-        if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
-        rb_block = blk;
-    }
-    rb_put(rb, q, r);
-}
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
 
@@ -552,10 +381,14 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) <<
 // stores dword k of the 72-byte icrc_rx_desc.
 __device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t hdr, uint64_t off, uint32_t L,
                                          uint32_t icrc_ok, uint32_t lane) {
-    // Wave-uniform part: BTH byte 0/1 and the header size decide the packet's shape.
-    const uint32_t w7 = __builtin_amdgcn_readlane(hdr, 7);
-    const uint32_t w9 = __builtin_amdgcn_readlane(hdr, 9);
-    const uint32_t w10 = __builtin_amdgcn_readlane(hdr, 10);
+    // Packet-wide values, broadcast into every lane with ds_bpermute rather than v_readlane: kept
+    // in VGPRs, they add no scalar-register pressure to the kernel around this epilogue.
+    auto bcast = [&](int w) __attribute__((always_inline)) {
+        return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(w << 2, static_cast<int>(hdr)));
+    };
+    const uint32_t w7 = bcast(7);
+    const uint32_t w9 = bcast(9);
+    const uint32_t w10 = bcast(10);
     const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
     // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
     const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
@@ -563,12 +396,11 @@ __device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t 
                       : (op == 0x11u)                 ? 16u
                       : (op >= 0x06u && op <= 0x10u)  ? 28u
                                                       : 0u;
-    uint32_t status;
-    if (L < ICRC_MIN_PACKET) status = ICRC_RX_TRUNCATED;
-    else if (hs == 0u) status = ICRC_RX_INVALID_OPCODE;
-    else if (tran > 6u) status = ICRC_RX_INVALID_TRANS_TYPE;
-    else if (L - 32u < hs + pad) status = ICRC_RX_TRUNCATED;  // buf_size = L - 28 - 4
-    else status = ICRC_RX_OK;
+    const uint32_t status = (L < ICRC_MIN_PACKET)   ? ICRC_RX_TRUNCATED
+                          : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
+                          : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
+                          : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
+                                                    : ICRC_RX_OK;
     const bool ack = hs == 16u;
     uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
                      (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
@@ -625,6 +457,203 @@ __device__ __forceinline__ uint32_t rx_header_bytes(const uint8_t *pkt, uint32_t
         }
     }
     return w;
+}
+
+// PARSE: gather packet words 0..17 into lanes 0..17 from the first two rows as loaded (raw, before
+// the ICRC masks): word w sits in row j, lane w + 1 - k0 - 64 j.
+__device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row1, int k0, uint32_t lane) {
+    const int s0 = static_cast<int>(lane) + 1 - k0;
+    const int s1 = s0 - 64;
+    const uint32_t v0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((s0 & 63) << 2, static_cast<int>(row0)));
+    const uint32_t v1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((s1 & 63) << 2, static_cast<int>(row1)));
+    return (s0 >= 0 && s0 < 64) ? v0 : ((s1 >= 0 && s1 < 64) ? v1 : 0u);
+}
+
+// Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
+// the wave's result buffer.
+template <int MODE, int S, int ABL, bool PARSE = false>
+__device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows],
+                                            uint32_t q0, ResultBuf &rb, uint32_t lo = 0) {
+    int rmax = 0;
+    bool same = true;  // every slot regular with the same row count (the common case)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (m[s].kind == 1 && m[s].R > rmax) rmax = m[s].R;
+        same = same && m[s].kind == 1 && m[s].R == m[0].R;
+    }
+    if (rmax > 0) {
+        uint32_t acc[S];
+        uint32_t hdr[S];  // PARSE: packet word w in lane w (w < 18), from rows 0 and 1 as loaded
+        if constexpr (PARSE) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) hdr[s] = rx_gather_header(u[s][0], u[s][1], m[s].k0, lane);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k = m[s].k0 + static_cast<int>(lane);
+            acc[s] = u[s][0] | head_mask(k);
+            u[s][1] |= head_mask(k + 64);
+        }
+        // One straight-line block per row for all S chains (the scheduler interleaves them).
+        if (same && rmax == kRows) {  // full-MTU packets (4 KiB): no per-row guard branches
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                    else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                }
+            }
+        } else if (same) {
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                        else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                    }
+                }
+            }
+        } else {
+            // a chain past its own last row keeps its value through a select
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (abl_mode(ABL) == 1) {
+                            acc[s] ^= u[s][j];
+                        } else {
+                            const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
+                            acc[s] = (j < m[s].R) ? t : acc[s];
+                        }
+                    }
+                }
+            }
+        }
+        uint32_t fin[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (m[s].kind == 1) {
+                const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
+                rb_put(rb, q0 + s, r);
+                if constexpr (PARSE)
+                    rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane);
+            }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (m[s].kind == 2) {
+            uint32_t hdr_slow = 0;
+            if constexpr (PARSE) hdr_slow = rx_header_bytes(m[s].pkt, m[s].L, lane);  // before any trailer zeroing
+            const uint32_t r = handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane);
+            rb_put(rb, q0 + s, r);
+            if constexpr (PARSE)
+                rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane);
+        }
+}
+
+// A wave owns the contiguous packet range [lo, lo + nq) and walks it in sets of S packets
+// (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
+// processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
+// ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
+template <int MODE, int S, int D, int ABL, bool PARSE = false>
+__device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                              uint32_t lane, uint32_t lo, uint32_t nq) {
+    constexpr int B = D + 1;
+    static_assert(64 % S == 0, "sets must not straddle a 64-packet result block");
+    if (nq == 0) return;
+    const uint32_t nsets = (nq + S - 1) / S;
+    const bool ragged = p.off != nullptr || p.len != nullptr;
+    MetaBlock mb;
+    mb.block = -1;
+    mb.off_lo = mb.off_hi = mb.len = 0;
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    SlotMeta m[B][S];
+    uint32_t u[B][S][kRows];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (static_cast<uint32_t>(d) < nsets) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                slot_meta(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
+                slot_load<ABL>(m[d][s], lane, u[d][s]);
+            }
+        }
+    }
+    for (uint32_t t = 0; t < nsets; t += B) {
+        const bool cont = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            const uint32_t ts = t + b;
+            if (ts >= nsets) return false;
+            const uint32_t tp = ts + D;
+            // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                slot_load<ABL>(m[bp][s], lane, u[bp][s]);
+            }
+            const uint32_t q0 = ts * S;
+            process_set<MODE, S, ABL, PARSE>(p, lds, c, lane, m[b], u[b], q0, rb, lo);
+            const uint32_t qn = q0 + S;  // next unprocessed
+            if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+            return true;
+        });
+        if (!cont) return;
+    }
+}
+
+// ---- row-stream path ------------------------------------------------------------------------
+// A wave's chunk is one flat sequence of 256-byte rows (the sum of R over its regular packets,
+// in packet order).  A ring of RD row loads stays in flight (RD * 256 B per wave); the
+// process side consumes rows in the same order, restarting the Horner accumulator at each
+// packet's first row and finalising at its last.  A short packet costs only its own rows,
+// a long one needs no special path, and every ring load is unconditional (exact vmcnt
+// accounting).  Misaligned packets and L % 4 != 0 are skipped by the stream and done by a
+// tail loop; L < 44 packets are recorded as errors when the process cursor passes them.
+struct RowCursor {  // wave-uniform
+    uint32_t q;     // packet sequence number within the chunk
+    int j;          // row within the packet
+    int R;          // rows of the current packet (0 = past the end)
+    int k0;
+    uint8_t *pkt;
+    uint32_t L;
+};
+
+// R >= 1: regular packet; 0: L < 44 (error); -1: irregular (generic path).
+__device__ __forceinline__ int classify(const uint8_t *pkt, uint32_t L, int &k0) {
+    if (L < ICRC_MIN_PACKET) return 0;
+    if (((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) != 0) return -1;
+    const int N = 1 + static_cast<int>((L - 4u) >> 2);
+    const int R = (N + 63) >> 6;
+    k0 = N - 64 * R;
+    return R;
+}
+
+__device__ __forceinline__ void meta_read(const MetaBlock &mb, uint32_t q, uint64_t &off, uint32_t &L) {
+    const int l = static_cast<int>(q & 63u);
+    off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
+          (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
+    L = __builtin_amdgcn_readlane(mb.len, l);
+}
+
+// Result buffer keyed by 64-packet block: switching block flushes the previous one.
+template <int MODE>
+__device__ __forceinline__ void rb_record(const BatchParams &p, ResultBuf &rb, int &rb_block, uint32_t lo,
+                                          uint32_t q, uint32_t r, uint32_t lane) {
+    const int blk = static_cast<int>(q >> 6);
+    if (blk != rb_block) {
+        if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+        rb_block = blk;
+    }
+    rb_put(rb, q, r);
 }
 
 template <int MODE, int RD, bool PARSE = false>
@@ -837,7 +866,8 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     }
 }
 
-// Receive: verify + strip + parse, the row stream with header capture (RD rows in flight).
+// Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
+// words gathered from each packet's first two rows.
 template <int RD>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
@@ -859,7 +889,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_rowstream<kVerify, RD, true>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, 1, 1, kStreamAux << 2, true>(p, lds, c, lane, lo, nq);
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------

@@ -38,16 +38,6 @@ def main():
 
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * L
     d_len = torch.full((n,), L, dtype=torch.int32, device="cuda")
-    eng.set_variant(10)  # row stream, ragged meta blocks: compute, then verify
-    d_out2 = torch.zeros(n, dtype=torch.int32, device="cuda")
-    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out2.data_ptr(), False, 0, s)
-    torch.cuda.synchronize()
-    say(f"stage 3a row-stream compute ragged ok: same={bool(torch.equal(d_out, d_out2))}")
-    d_ok.zero_()
-    eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), False, 0, s)
-    torch.cuda.synchronize()
-    say(f"stage 3b row-stream verify ragged ok: all_ok={bool((d_ok == 1).all().item())}")
-    eng.set_variant(-1)
     d_ok.zero_()
     eng.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(), d_ok.data_ptr(), stream=s)
     torch.cuda.synchronize()
@@ -85,6 +75,27 @@ def main():
                  stream=s)
     torch.cuda.synchronize()
     say(f"stage 6 rx over packetized wire ok: all_ok={bool((d_ok == 1).all().item())}")
+    del d_src, d_wire, d_desc
+    torch.cuda.empty_cache()
+    # row-stream variants (10-12) at C1 size with offset/length arrays
+    w = workloads.write_middle_stream(n, 4096)
+    d_buf = workloads.synthesize(eng, w, stream=s)
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * L
+    d_len = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out.data_ptr(), True, 0, s)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    eng.set_variant(10)  # row stream, ragged meta blocks: compute, then verify
+    d_out2 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out2.data_ptr(), False, 0, s)
+    torch.cuda.synchronize()
+    say(f"stage 3a row-stream compute ragged ok: same={bool(torch.equal(d_out, d_out2))}")
+    d_ok.zero_()
+    eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), False, 0, s)
+    torch.cuda.synchronize()
+    say(f"stage 3b row-stream verify ragged ok: all_ok={bool((d_ok == 1).all().item())}")
+    eng.set_variant(-1)
     return 0
 
 
