@@ -295,6 +295,15 @@ struct MetaBlock {
     int block;                     // uniform
 };
 
+// v_readlane as an unsigned value (the builtin returns int: widening it directly to 64 bits
+// sign-extends offsets >= 2 GiB).
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+}
+__device__ __forceinline__ uint64_t meta_off(const MetaBlock &mb, int l) {
+    return static_cast<uint64_t>(readlane_u32(mb.off_lo, l)) | (static_cast<uint64_t>(readlane_u32(mb.off_hi, l)) << 32);
+}
+
 __device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, uint32_t lo, uint32_t hi,
                                            int block, uint32_t lane) {
     const uint32_t i = lo + static_cast<uint32_t>(block) * 64u + lane;
@@ -324,9 +333,8 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
         const int block = static_cast<int>(q >> 6);
         if (block != mb.block) meta_fetch(p, mb, lo, lo + nq, block, lane);
         const int l = static_cast<int>(q & 63u);
-        off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
-              (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
-        L = __builtin_amdgcn_readlane(mb.len, l);
+        off = meta_off(mb, l);
+        L = readlane_u32(mb.len, l);
     } else {
         off = static_cast<uint64_t>(lo + q) * p.stride;
         L = p.ulen;
@@ -661,9 +669,8 @@ __device__ __forceinline__ int classify(const uint8_t *pkt, uint32_t L, int &k0)
 
 __device__ __forceinline__ void meta_read(const MetaBlock &mb, uint32_t q, uint64_t &off, uint32_t &L) {
     const int l = static_cast<int>(q & 63u);
-    off = static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_lo, l)) |
-          (static_cast<uint64_t>(__builtin_amdgcn_readlane(mb.off_hi, l)) << 32);
-    L = __builtin_amdgcn_readlane(mb.len, l);
+    off = meta_off(mb, l);
+    L = readlane_u32(mb.len, l);
 }
 
 // Result buffer keyed by 64-packet block: switching block flushes the previous one.
@@ -938,7 +945,7 @@ struct MsgRegs {  // the 88-byte icrc_write_msg, one dword per lane (lanes 0..21
     int idx;  // uniform: message index held, -1 = none
 };
 
-__device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return __builtin_amdgcn_readlane(m.v, dw); }
+__device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return readlane_u32(m.v, dw); }
 __device__ __forceinline__ uint64_t msg_u64(const MsgRegs &m, int dw) {
     return static_cast<uint64_t>(msg_u32(m, dw)) | (static_cast<uint64_t>(msg_u32(m, dw + 1)) << 32);
 }

@@ -587,3 +587,45 @@ def test_ipv4_checksum_reference_vectors_and_fill(engine):
         assert int(got[i]) == c
         h = filled[int(o): int(o) + 20]
         assert (int(h[10]) << 8 | int(h[11])) == c and oracle.ipv4_checksum(h) == 0
+
+
+def test_ragged_offsets_beyond_2GiB(engine):
+    """Offset arrays with entries >= 2^31 and >= 2^32 (v_readlane returns int: widening it must not
+    sign-extend): compute, verify and receive-parse against the oracle."""
+    import icrc_amd
+
+    rng = np.random.default_rng(44)
+    pkts, _ = [], None
+    for i in range(300):
+        L = int(rng.choice([44, 316, 1084, 4156, 4157, 777]))
+        pkts.append(rng.integers(0, 256, L, dtype=np.uint8))
+    total = (1 << 32) + (1 << 20)
+    d_buf = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    starts = [(1 << 31) - 5000, (1 << 32) - 3000]
+    off, pos = [], 0
+    for i, p in enumerate(pkts):
+        base = starts[i % 2] + (i // 2) * 4200
+        off.append(base)
+        d_buf[base: base + p.size] = torch.from_numpy(p).cuda()
+    off = np.asarray(off, np.uint64)
+    lens = np.asarray([p.size for p in pkts], np.uint32)
+    d_off, d_len = dev(off), dev(lens)
+    n = len(pkts)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out.data_ptr(), True, 0,
+                         stream_handle())
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), False, 0,
+                        stream_handle())
+    d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+    engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(), stream=stream_handle())
+    torch.cuda.synchronize()
+    want = [oracle.compute_icrc(p) for p in pkts]
+    assert [int(x) for x in d_out.cpu().numpy().view(np.uint32)] == want
+    assert d_ok.cpu().numpy().tolist() == [1] * n
+    desc = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+    assert np.all(desc["icrc_ok"] == 1)
+    ok_parse = desc["status"] == 0
+    assert np.all(desc["payload_offset"][ok_parse] >= np.asarray(off)[ok_parse] + 28)
+    del d_buf
+    torch.cuda.empty_cache()
