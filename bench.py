@@ -53,6 +53,26 @@ def parse():
     return ap.parse_args()
 
 
+PMC_TRAFFIC_FILE = "r01_pmc_traffic.json"
+
+
+def pmc_traffic(n: int, L: int):
+    """roofline.traffic: HBM bytes per launch of the ICRC kernel from rocprofv3 PMC passes
+    (FETCH_SIZE and WRITE_SIZE in separate runs of this same bench command, FETCH_SIZE corrected
+    by the membench calibration; scripts/gpu_check.sh PMC=1 -> scripts/pmc_summary.py).  A bench
+    process cannot read its own counters, so the committed summary is used when it was taken on
+    this exact workload; otherwise None."""
+    path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
+    try:
+        with open(path) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if tr.get("packets") != n or tr.get("packet_bytes") != L:
+        return None
+    return tr
+
+
 def dev(a: np.ndarray) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
 
@@ -148,6 +168,12 @@ def main() -> int:
             "kernel_ms": round(kms, 4),
         },
     }
+    tr = pmc_traffic(n, L)
+    if tr is not None:
+        result["roofline"]["traffic"] = tr["traffic_bytes"]
+        result["roofline"]["traffic_source"] = (
+            f"profiles/{PMC_TRAFFIC_FILE}: {tr['kernel']} HBM bytes per launch (FETCH_SIZE x "
+            f"{tr['fetch_correction']} + WRITE_SIZE), {tr['ratio_to_algorithmic']}x the algorithmic bytes")
 
     # ---- CPU baseline: rank 0, N = 1 only ----
     parity = True

@@ -1,19 +1,31 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/gpu_pmc.sh).
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/gpu_check.sh PMC=1).
 
-Per kernel name: mean counter value per dispatch (KB, summed over the counter's instances),
-converted to bytes.  For membench dispatches the algorithmic read bytes are known
-(1 Mi x 4156 B, or L-4 per packet for the row patterns), which gives the FETCH_SIZE
-calibration factor for these access widths (MI355X_MICROARCH.md: FETCH_SIZE under-reports
-wide streaming reads by 2x on gfx950; other widths must be calibrated)."""
+Per kernel: mean counter value per dispatch (KB, summed over the counter's instances), in bytes.
+For the membench dispatches the algorithmic read bytes are known (1 Mi x 4156 B, or L-4 per
+packet for the row patterns), which calibrates FETCH_SIZE for these access widths on gfx950
+(MI355X_MICROARCH.md, HBM section: FETCH_SIZE reports 1/2 of the bytes of a wide streaming read;
+other widths must be calibrated on a known byte count).
+
+The `icrc_traffic_per_launch` block is what bench.py reports as roofline.traffic: the ICRC
+compute kernel's corrected FETCH bytes + WRITE bytes per launch over the C1 batch."""
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 N, L = 1 << 20, 4156
+
+
+def short(name):
+    """'void icrc::(anonymous namespace)::icrc_batch_kernel<0, 1, 1, 8>(icrc::BatchParams)' ->
+    'icrc_batch_kernel<0, 1, 1, 8>'"""
+    head = re.sub(r"^void ", "", name.replace("(anonymous namespace)", "anon").split("(")[0])
+    base, sep, tmpl = head.partition("<")
+    return base.split("::")[-1] + sep + tmpl
 
 
 def load(pattern):
@@ -30,7 +42,7 @@ def load(pattern):
             acc[key] += float(r.get("Counter_Value", 0) or 0)
             names[key] = r.get("Kernel_Name", "?")
         for k, v in acc.items():
-            per[names[k]].append(v)
+            per[short(names[k])].append(v)
     return per
 
 
@@ -41,8 +53,7 @@ def main():
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             per = load(os.path.join(out, f"pmc_{src}_{c}", "**", "*.csv"))
             for name, vals in per.items():
-                short = name.split("(")[0][-80:]
-                d = res.setdefault(src, {}).setdefault(short, {})
+                d = res.setdefault(src, {}).setdefault(name, {})
                 d[c + "_KB_mean"] = sum(vals) / len(vals)
                 d[c + "_KB_min"] = min(vals)
                 d["dispatches_" + c] = len(vals)
@@ -56,15 +67,19 @@ def main():
     res["fetch_calibration_bytes_per_counted_byte"] = factors
     bench = res.get("bench", {})
     for name, d in bench.items():
-        if "icrc_batch_kernel" in name and "FETCH_SIZE_KB_mean" in d:
+        if name.startswith("icrc_batch_kernel<0,") and "FETCH_SIZE_KB_mean" in d:
+            # the kernel's own shape (256-B dword rows per wave) is membench's rows_chunk / rows_dword
             f = [v for k, v in factors.items() if "rows_chunk" in k or "rows_dword" in k]
             corr = sum(f) / len(f) if f else 2.0
             fetch = d["FETCH_SIZE_KB_mean"] * 1024.0 * corr
             write = d.get("WRITE_SIZE_KB_mean", 0.0) * 1024.0
+            alg = N * L
             res["icrc_traffic_per_launch"] = {
-                "kernel": name, "fetch_bytes_corrected": fetch, "write_bytes": write,
-                "traffic_bytes": fetch + write, "algorithmic_bytes": N * L,
-                "ratio_to_algorithmic": (fetch + write) / (N * L), "fetch_correction": corr}
+                "kernel": name, "packets": N, "packet_bytes": L,
+                "fetch_bytes_counted": d["FETCH_SIZE_KB_mean"] * 1024.0,
+                "fetch_correction": round(corr, 4), "fetch_bytes_corrected": round(fetch),
+                "write_bytes": round(write), "traffic_bytes": round(fetch + write),
+                "algorithmic_bytes": alg, "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
     print(json.dumps(res, indent=1))
 
 
