@@ -70,8 +70,10 @@ int icrc_engine_default(int device, icrc_engine **out);
 int icrc_engine_device_ordinal(const icrc_engine *engine);
 /* The engine's own non-blocking stream (a hipStream_t), for callers without one. */
 void *icrc_engine_stream(const icrc_engine *engine);
-/* Tuning knob for A/B measurement: 0 = one packet per wavefront at a time, S >= 1 = software-
- * pipelined with S packets in flight per wavefront; -1 = the default.  Results are identical. */
+/* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode): 0 = one packet
+ * per wavefront at a time, 1..18 = one packet per wavefront, software-pipelined, 19..21 = four
+ * packets per wavefront; -1 = the defaults (13 for uniform strided batches, 20 for ragged ones).
+ * Results are identical. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
 int icrc_device_count(void);
@@ -292,6 +294,9 @@ int icrc_rdma_header_len(uint8_t opcode);
 /* ---- host-only helpers (no GPU needed) -------------------------------------------------- */
 /* The 160 KiB LDS table image the kernel uploads (layout documented in DESIGN.md). */
 int icrc_table_image(uint32_t *out_words, uint32_t nwords);
+/* The quad kernel's image (four packets per wavefront): M^16 bulk tables, M^(16 - (l & 15))
+ * final tables, same layout. */
+int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords);
 
 #ifdef __cplusplus
 }

@@ -39,8 +39,9 @@ struct Stage {
 struct icrc_engine {
     int device = 0;
     int num_cu = 0;
-    int variant = icrc::kDefaultVariant;
+    int variant = -1;  // -1: kDefaultVariant for strided batches, kDefaultRaggedVariant otherwise
     uint32_t *d_table = nullptr;
+    uint32_t *d_table_quad = nullptr;
     hipStream_t stream = nullptr;
     std::mutex mu;  // guards the host-batch stages
     Stage st[2];
@@ -67,6 +68,13 @@ struct DeviceGuard {
     do {                                               \
         if ((expr) != hipSuccess) return ICRC_EDEVICE; \
     } while (0)
+
+// Kernel variant of a batch: the engine's forced variant, else the default for its shape (the
+// one-packet-per-wavefront pipeline for uniform strided batches, the quad kernel for ragged).
+int variant_for(const icrc_engine *e, bool ragged) {
+    if (e->variant >= 0) return e->variant;
+    return ragged ? icrc::kDefaultRaggedVariant : icrc::kDefaultVariant;
+}
 
 int grid_for(const icrc_engine *e, uint32_t n) {
     const uint64_t want = (static_cast<uint64_t>(n) + icrc::kWavesPerGroup - 1) / icrc::kWavesPerGroup;
@@ -256,8 +264,9 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
         p.len = s.d_len;
         p.n = cnt;
         p.table = e->d_table;
+        p.table_quad = e->d_table_quad;
         p.trailer = 0;  // trailers are applied to the caller's host copy in finish_stage
-        p.variant = e->variant;
+        p.variant = variant_for(e, true);
         if (mode == icrc::kCompute) p.out = s.d_res;
         else p.ok = reinterpret_cast<uint8_t *>(s.d_res);
         if ((rc = icrc::launch_batch(mode, p, grid_for(e, cnt), s.stream)) != ICRC_OK) break;
@@ -299,8 +308,9 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     p.ok = d_ok;
     p.nerr = d_nerr;
     p.table = e->d_table;
+    p.table_quad = e->d_table_quad;
     p.trailer = trailer ? 1 : 0;
-    p.variant = e->variant;
+    p.variant = variant_for(e, d_off != nullptr || d_len != nullptr);
     return icrc::launch_batch(mode, p, grid_for(e, n), stream);
 }
 
@@ -339,10 +349,13 @@ int icrc_engine_create(int device, icrc_engine **out) {
         return ICRC_EDEVICE;
     }
     e->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
-    std::vector<uint32_t> img(icrc::kLdsWords);
+    std::vector<uint32_t> img(icrc::kLdsWords), img_quad(icrc::kLdsWords);
     icrc::build_table_image(img.data());
+    icrc::build_table_image_quad(img_quad.data());
     if (hipMalloc(&e->d_table, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table, img.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&e->d_table_quad, icrc::kLdsBytes) != hipSuccess ||
+        hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         icrc_engine_destroy(e);
         return ICRC_EDEVICE;
@@ -358,6 +371,7 @@ int icrc_engine_destroy(icrc_engine *e) {
         if (e->stream) (void)hipStreamSynchronize(e->stream);
         for (Stage &s : e->st) stage_free(s);
         if (e->d_table) (void)hipFree(e->d_table);
+        if (e->d_table_quad) (void)hipFree(e->d_table_quad);
         if (e->stream) (void)hipStreamDestroy(e->stream);
     }
     {
@@ -396,7 +410,7 @@ int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : IC
 
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
     if (!e || variant < -1 || variant > icrc::kMaxVariant) return ICRC_EINVAL;
-    e->variant = variant < 0 ? icrc::kDefaultVariant : variant;
+    e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;
 }
 
@@ -574,6 +588,12 @@ int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t s
 int icrc_table_image(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image(out_words);
+    return ICRC_OK;
+}
+
+int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords) {
+    if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
+    icrc::build_table_image_quad(out_words);
     return ICRC_OK;
 }
 

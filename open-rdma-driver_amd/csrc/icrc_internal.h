@@ -19,6 +19,11 @@ constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
 // Host: fill a kLdsWords image.
 void build_table_image(uint32_t *img);
+// Quad image (the 4-packets-per-wavefront kernel, 16 lanes = 16 stream words per packet row):
+// the same layout with M^16 in the bulk tables and, for lane l, M^(16 - (l & 15)) in the
+// final tables — so the final lookup of lane l = 16 g + c is conflict-free across the 4
+// packet groups g (bank (16 g + c) of each 256-byte table row).
+void build_table_image_quad(uint32_t *img);
 // Host reference helpers used by the table builder (exposed for unit tests).
 uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
 
@@ -37,10 +42,13 @@ struct BatchParams {
     int trailer;     // compute: write trailer; verify: zero trailer
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
+    const uint32_t *table_quad;  // kLdsWords quad image (variants >= kFirstQuadVariant)
 };
 
 constexpr int kDefaultVariant = 13;  // S=1, D=1, nt row loads (A/B: profiles/r01_ab_nt.json)
-constexpr int kMaxVariant = 18;
+constexpr int kFirstQuadVariant = 19;  // 19..21: 4 packets per wavefront (chunk pipeline, K x D)
+constexpr int kDefaultRaggedVariant = 20;
+constexpr int kMaxVariant = 21;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 
@@ -50,6 +58,8 @@ constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
 // Launch wrappers (icrc_kernels.hip).  `grid` = number of workgroups.
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
 int launch_rx(const BatchParams &p, int grid, void *stream);  // verify + parse (p.rx)
+// Quad kernel (icrc_quad.hip), variant 19..21 (chunk size / chunks in flight).
+int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {

@@ -1,0 +1,471 @@
+// icrc_quad.hip — the four-packets-per-wavefront ICRC kernel (variants 19-21, the default for
+// ragged batches).  Bit-exact with compute_icrc / is_icrc_valid
+// (blue-rdma-device/src/third_party/net/packet_processor.rs:275-301, 341-353); the algorithm is
+// described at the top of icrc_kernels.hip, the quad mapping below.
+#include <hip/hip_runtime.h>
+
+#include "icrc_device.h"
+#include "icrc_internal.h"
+
+namespace icrc {
+namespace {
+
+// ---- quad path: four packets per wavefront ------------------------------------------------
+// Lanes 16g .. 16g+15 (group g = lane >> 4, column c = lane & 15) carry one packet.  A packet
+// row is 16 stream words (one buffer_load_dword per lane: 64 contiguous bytes per group, 256 B
+// per wave instruction); rows are end-aligned as in the one-packet path, so the column
+// multiplier M^(16-c) depends only on the lane.  Tables: the quad image (M^16 bulk, M^(16-c)
+// final; build_table_image_quad).  Against one packet per wavefront this divides every
+// per-packet cost (final multiply, reduction, result handling) by four and cuts the padding
+// of short packets from up to 63 words to up to 15: the mixed-MTU batch is dominated by
+// 316-byte packets (79 stream words: 5 quad rows, 80 slots, against 2 x 64 = 128).
+//
+// A wave walks its chunk in blocks of 64 packets.  Each block is sorted by row count (bitonic
+// sort of (R << 6 | index) across the lanes), and consecutive sorted packets form sets of 4
+// processed in lockstep; a shorter packet in a set is END-aligned to the longest by leading
+// zero rows, which leave a zero accumulator at zero, so no guards are needed.  Packets
+// outside the fast path (L < 44, misaligned, L % 4 != 0, offsets too far apart for 32-bit
+// buffer offsets) are done by a tail loop.
+constexpr uint32_t kQuadOOR = 0x80000000u;        // voffset past the range: the load returns 0
+constexpr uint32_t kQuadRelLimit = 0x7F000000u;   // packet offset in its block + L stay below
+constexpr uint32_t kQuadIrregular = 0x3FFFFFFu;   // sort key (>> 6) of a non-fast-path slot
+constexpr int kQuadEmptyE = -(1 << 30);          // word index of a group with no packet
+
+__device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
+}
+
+// XOR over each 16-lane row (DPP quad_perm x2, row_ror 4, 8): every lane gets its group's XOR.
+__device__ __forceinline__ uint32_t group_xor(uint32_t x) {
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x124, 0xF, 0xF, false));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x128, 0xF, 0xF, false));
+    return x;
+}
+
+struct QuadBlock {
+    uint32_t key;   // per lane p (sorted position): R << 6 | block index of the packet
+    uint32_t vrel;  // per lane p: packet offset relative to the block's buffer base
+    uint32_t len;   // per lane p: L
+    uint32_t pos;   // per lane i (block index): sorted position of packet i
+    uint64_t regmask;  // uniform: block indices of fast-path packets
+    uint64_t boff;     // uniform: buffer base (byte offset from p.base)
+    int block;         // uniform
+    int nsets;         // uniform
+};
+
+struct QuadSet {
+    uint32_t vb;  // per lane: byte offset of this lane's word in set row 0 (mod 2^32)
+    int e;        // per lane: packet word index at set row 0 (< 0: before the packet)
+    int rows;     // uniform: rows of the longest packet in the set
+    int hrows;    // uniform: rows that may hold header words (head masks / OOR selects)
+};
+
+// Fast-path classification of block b's packets (off, L of this lane's packet) and the block's
+// buffer base.  Returns the ballot of the valid packets that are NOT on the fast path.
+__device__ __forceinline__ uint64_t quad_classify_from(const BatchParams &p, uint64_t off, uint32_t L, bool valid,
+                                                       uint32_t lo, int b, uint32_t lane, bool &reg, uint64_t &boff) {
+    reg = valid && L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(p.base + off) | L) & 3u) == 0;
+    if (p.off == nullptr) {
+        boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(b) * 64u) * p.stride;
+    } else {  // minimum offset over the fast-path packets (64-bit butterfly)
+        uint64_t m = reg ? off : ~0ull;
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint32_t pl = lane ^ static_cast<uint32_t>(s);
+            const uint64_t o = static_cast<uint64_t>(bperm(pl, static_cast<uint32_t>(m))) |
+                               (static_cast<uint64_t>(bperm(pl, static_cast<uint32_t>(m >> 32))) << 32);
+            m = o < m ? o : m;
+        }
+        boff = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(m), 0)) |
+               (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(m >> 32), 0)) << 32);
+    }
+    reg = reg && (off - boff) + L <= kQuadRelLimit;
+    return __ballot(valid && !reg);
+}
+
+// The same, reading (offset, L) from the batch arrays (tail loop).
+__device__ __forceinline__ uint64_t quad_classify(const BatchParams &p, uint32_t lo, uint32_t nq, int b,
+                                                  uint32_t lane, uint64_t &off, uint32_t &L, bool &reg,
+                                                  uint64_t &boff) {
+    const uint32_t q = static_cast<uint32_t>(b) * 64u + lane;
+    const bool valid = q < nq;
+    const uint32_t i = lo + q;
+    off = 0;
+    L = 0;
+    if (valid) {
+        off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
+        L = p.len ? p.len[i] : p.ulen;
+    }
+    return quad_classify_from(p, off, L, valid, lo, b, lane, reg, boff);
+}
+
+// Block b: classification, then the fast-path packets sorted by row count (bitonic sort of
+// R << 6 | index across the lanes; skipped when already sorted).
+__device__ __forceinline__ void quad_block_from(const BatchParams &p, QuadBlock &B, uint64_t off, uint32_t L,
+                                                bool valid, uint32_t lo, int b, uint32_t lane, bool &irregular) {
+    uint64_t boff;
+    bool reg;
+    if (quad_classify_from(p, off, L, valid, lo, b, lane, reg, boff) != 0) irregular = true;
+    const uint32_t R = reg ? (1u + ((L - 4u) >> 2) + 15u) >> 4 : kQuadIrregular;
+    uint32_t key = (R << 6) | lane;
+    const uint32_t nxt = bperm((lane + 1u) & 63u, key);
+    if (__ballot(lane == 63u || key <= nxt) != ~0ull) {
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t other = bperm(lane ^ static_cast<uint32_t>(j), key);
+                const bool up = (lane & static_cast<uint32_t>(k)) == 0u;
+                const bool lower = (lane & static_cast<uint32_t>(j)) == 0u;
+                const uint32_t mn = key < other ? key : other;
+                const uint32_t mx = key < other ? other : key;
+                key = (lower == up) ? mn : mx;
+            }
+        }
+    }
+    const uint32_t idx = key & 63u;
+    B.key = key;
+    B.vrel = bperm(idx, static_cast<uint32_t>(off - boff));
+    B.len = bperm(idx, L);
+    B.pos = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>(idx << 2), static_cast<int>(lane)));
+    B.regmask = __ballot(reg);
+    B.boff = boff;
+    B.block = b;
+    B.nsets = (__popcll(B.regmask) + 3) >> 2;
+}
+
+__device__ __forceinline__ void quad_set(const QuadBlock &B, int s, uint32_t lane, QuadSet &S) {
+    const int nreg = __popcll(B.regmask);
+    const uint32_t ps = static_cast<uint32_t>(4 * s) + (lane >> 4);
+    const uint32_t key = bperm(ps & 63u, B.key);
+    const uint32_t vrel = bperm(ps & 63u, B.vrel);
+    const uint32_t L = bperm(ps & 63u, B.len);
+    const int last = (4 * s + 3 < nreg) ? 4 * s + 3 : nreg - 1;
+    const int Rmax = static_cast<int>(readlane_u32(B.key, last) >> 6);
+    const int Rmin = static_cast<int>(readlane_u32(B.key, 4 * s) >> 6);
+    const int R = static_cast<int>(key >> 6);
+    const int N = 1 + static_cast<int>((L - 4u) >> 2);
+    const int k0 = N - 16 * R;
+    const bool valid = static_cast<int>(ps) < nreg;
+    S.e = valid ? k0 - 1 + static_cast<int>(lane & 15u) - 16 * (Rmax - R) : kQuadEmptyE;
+    S.vb = vrel + 4u * static_cast<uint32_t>(S.e);
+    S.rows = Rmax;
+    const int full = 4 * s + 3 < nreg;
+    S.hrows = full ? (Rmax - Rmin + 2 < Rmax ? Rmax - Rmin + 2 : Rmax) : Rmax + 1;
+}
+
+// Generic per-packet path on the quad tables (group 0 computes; wave-uniform result).
+template <int MODE>
+__device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
+                                                     const LaneConsts &c, uint32_t lane) {
+    if (L < ICRC_MIN_PACKET) {
+        if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
+        return MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN;
+    }
+    const uint32_t Ld = L - 4u;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
+    const uint32_t T = 4u + Ld;
+    const int z = static_cast<int>((4u - (T & 3u)) & 3u);
+    const int N = static_cast<int>((T + static_cast<uint32_t>(z)) >> 2);
+    const int R = (N + 15) >> 4;
+    const int k0 = N - 16 * R;
+    const int col = static_cast<int>(lane & 15u);
+    const bool g0 = lane < 16u;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pkt, 0, aligned ? static_cast<int>(Ld) : 0, 0x00020000);
+    uint32_t acc = 0;
+    for (int r = 0; r < R; ++r) {
+        const int k = k0 + 16 * r + col;
+        uint32_t u;
+        if (aligned) {
+            u = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(4u * static_cast<uint32_t>(k - 1)), 0, 0);
+            u |= head_mask(k);
+        } else {
+            u = g0 ? slow_word(pkt, k, z) : 0u;
+        }
+        u = g0 ? u : 0u;
+        acc = step_m64(lds, acc, u, c);
+    }
+    const uint32_t crc = ~readlane_u32(group_xor(final_mul(lds, acc, c.fin)), 0);
+    return packet_result<MODE>(p, pkt, Ld, crc, aligned, lane);
+}
+
+// Chunk pipeline.  A set's rows (end-aligned, see above) are cut into chunks of K rows, the
+// first chunk padded in front with rows that load nothing (leading zeros: free), so every
+// chunk is K straight-line loads and K straight-line steps.  A ring of B = D + 1 chunk buffers
+// keeps D chunks in flight per wavefront; every buffer carries the metadata the process side
+// needs (word index for head masks, last-chunk flag, trailer offset, result routing, block),
+// so the process side holds no block state however far the load side has run ahead.  Every
+// ring position issues exactly the same loads (absent rows have an out-of-range offset), and
+// a ragged batch's next-block (offset, len) is loaded once per ring cycle, unconditionally:
+// the compiler's vmcnt accounting stays exact and no wait drains the ring.
+
+template <int MODE, int K, int D, bool RAGGED, bool TRAILER>
+__device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
+                                         uint32_t lo, uint32_t nq) {
+    constexpr int B = D + 1;
+    constexpr int KT = MODE == kVerify ? K + 1 : K;  // verify: + the stored trailers
+    if (nq == 0) return;
+    const int nblocks = static_cast<int>((nq + 63u) >> 6);
+    const uint32_t grp = lane >> 4;
+    const uint32_t col = lane & 15u;
+    bool irregular = false;
+
+    // Next block NB, prepared at the top of a ring cycle (one copy of the sort, not B), from
+    // the (offset, len) registers loaded at the top of the cycle before (ragged batches).
+    QuadBlock NB;
+    int nb_next = 0, mblk = -1;
+    bool nb_ready = false;
+    uint32_t m_lo = 0, m_hi = 0, m_len = 0;
+
+    // load side
+    QuadBlock LB;
+    QuadSet LS;
+    int lblk = -1, lset = 0, f = 0;
+    bool lhave = false, ldone = false;
+    int inflight = 0;
+
+    // ring: data and carried metadata
+    uint32_t u[B][KT];
+    uint32_t ce[B];   // per lane: (word index at chunk row 0, clamped) << 8 | result route (0xFF none)
+    uint32_t ctr[B];  // per lane: trailer offset (TRAILER only)
+    int cflags[B];    // uniform: bit 31 valid, bit 30 last chunk of its set, bits 0..7 head rows
+    int cblk[B];
+    uint64_t cboff[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        cflags[b] = 0;
+        cblk[b] = -1;
+        cboff[b] = 0;
+        ce[b] = 0xFFu;
+        ctr[b] = kQuadOOR;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) u[b][j] = 0;
+    }
+
+    // process side
+    uint32_t acc = 0, rbv = 0;
+    bool got = false;
+    int rb_block = -1;
+
+    // load side of one ring position: the next chunk (or nothing) into buffer b
+    auto l_issue = [&](auto bc) __attribute__((always_inline)) {
+        constexpr int b = decltype(bc)::value;
+        if (!lhave && !ldone) {  // next set: in this block, else the prepared next block
+            bool ok = false;
+            if (lblk >= 0 && lset + 1 < LB.nsets) {
+                lset += 1;
+                ok = true;
+            } else if (nb_ready) {
+                LB = NB;
+                nb_ready = false;
+                lblk = LB.block;
+                lset = 0;
+                ok = true;
+            } else if (nb_next >= nblocks) {
+                ldone = true;
+            }  // else a stall: the next block is prepared at the top of the next cycle
+            if (ok) {
+                quad_set(LB, lset, lane, LS);
+                f = LS.rows - ((LS.rows + K - 1) / K) * K;
+                lhave = true;
+            }
+        }
+        int fl = 0;
+        uint32_t vb = 0;
+        if (lhave) {
+            vb = LS.vb + 64u * static_cast<uint32_t>(f);
+            const int hr = LS.hrows - f;
+            fl = (1 << 31) | (hr < 0 ? 0 : (hr > K ? K : hr));
+            const bool last = f + K >= LS.rows;
+            if (last) fl |= 1 << 30;
+            const uint32_t ps = LB.pos;
+            const bool mine = last && ((LB.regmask >> lane) & 1ull) && static_cast<int>(ps >> 2) == lset;
+            const int e = LS.e + 16 * f;
+            ce[b] = (static_cast<uint32_t>(e < -(1 << 20) ? -(1 << 20) : e) << 8) | (mine ? (ps & 3u) << 4 : 0xFFu);
+            if constexpr (TRAILER) {
+                ctr[b] = (col == 0u && LS.e != kQuadEmptyE) ? LS.vb + 64u * static_cast<uint32_t>(LS.rows) : kQuadOOR;
+            }
+            cblk[b] = lblk;
+            cboff[b] = LB.boff;
+        }
+        const __amdgpu_buffer_rsrc_t lrs =
+            __builtin_amdgcn_make_buffer_rsrc(p.base + LB.boff, 0, static_cast<int>(kQuadOOR), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int r = f + j;
+            uint32_t vo = kQuadOOR;
+            if (lhave && r >= 0) {
+                vo = vb + 64u * static_cast<uint32_t>(j);
+                if (r < LS.hrows) vo = (LS.e + 16 * r >= 0) ? vo : kQuadOOR;
+            }
+            u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kStreamAux);
+        }
+        if constexpr (MODE == kVerify) {  // lane 16 g: packet g's stored ICRC (the set's last chunk)
+            const bool t = lhave && (fl & (1 << 30)) && col == 0u && LS.e != kQuadEmptyE;
+            const uint32_t vo = t ? LS.vb + 64u * static_cast<uint32_t>(LS.rows) : kQuadOOR;
+            u[b][K] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kStreamAux);
+        }
+        cflags[b] = fl;
+        if (lhave) {
+            inflight += 1;
+            f += K;
+            if (f >= LS.rows) lhave = false;
+        }
+    };
+
+    // process side of one ring position: buffer b
+    auto p_consume = [&](auto bc) __attribute__((always_inline)) {
+        constexpr int b = decltype(bc)::value;
+        const int fl = cflags[b];
+        if (!(fl & (1 << 31))) return;
+        const int hr = fl & 0xFF;
+        const int e = static_cast<int>(ce[b]) >> 8;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            uint32_t x = u[b][j];
+            if (j < hr) x |= head_mask(e + 16 * j + 1);
+            acc = step_m64(lds, acc, x, c);
+        }
+        inflight -= 1;
+        if (fl & (1 << 30)) {
+            const uint32_t crc = ~group_xor(final_mul(lds, acc, c.fin));
+            acc = 0;
+            uint32_t r;
+            if constexpr (MODE == kCompute) r = crc;
+            else r = bperm(grp << 4, u[b][K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+            if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(p.base + cboff[b], 0, static_cast<int>(kQuadOOR), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs, static_cast<int>(ctr[b]), 0, 0);
+            }
+            if (cblk[b] != rb_block) {
+                if (rb_block >= 0 && got) store_result<MODE>(p, lo + static_cast<uint32_t>(rb_block) * 64u + lane, rbv);
+                got = false;
+                rb_block = cblk[b];
+            }
+            const uint32_t rt = ce[b] & 0xFFu;
+            const uint32_t v = bperm(rt & 63u, r);
+            if (rt != 0xFFu) {
+                rbv = v;
+                got = true;
+            }
+        }
+    };
+
+    for (;;) {
+        // top of the cycle: prepare the next block, then fetch the (offset, len) of the one after
+        if (!nb_ready && nb_next < nblocks && (!RAGGED || mblk == nb_next)) {
+            const uint32_t q = static_cast<uint32_t>(nb_next) * 64u + lane;
+            const bool valid = q < nq;
+            uint64_t off = 0;
+            uint32_t L = 0;
+            if (valid) {
+                off = p.off ? (static_cast<uint64_t>(m_lo) | (static_cast<uint64_t>(m_hi) << 32))
+                            : static_cast<uint64_t>(lo + q) * p.stride;
+                L = p.len ? m_len : p.ulen;
+            }
+            quad_block_from(p, NB, off, L, valid, lo, nb_next, lane, irregular);
+            nb_next += 1;
+            nb_ready = NB.nsets > 0;
+        }
+        if constexpr (RAGGED) {  // unconditional: one load pair per cycle keeps vmcnt exact
+            const uint32_t q = static_cast<uint32_t>(nb_next) * 64u + lane;
+            const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint64_t *>(p.off ? p.off + lo : nullptr), 0, p.off ? static_cast<int>(nq * 8u) : 0, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs_len = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(p.len ? p.len + lo : nullptr), 0, p.len ? static_cast<int>(nq * 4u) : 0, 0x00020000);
+            const auto o = __builtin_amdgcn_raw_buffer_load_b64(rs_off, static_cast<int>(q * 8u), 0, 0);
+            m_lo = o[0];
+            m_hi = o[1];
+            m_len = __builtin_amdgcn_raw_buffer_load_b32(rs_len, static_cast<int>(q * 4u), 0, 0);
+            mblk = nb_next;
+        }
+        static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            l_issue(IntC<(b + D) % B>{});
+            p_consume(bc);
+            return true;
+        });
+        if (ldone && inflight == 0) break;
+    }
+    if (rb_block >= 0 && got) store_result<MODE>(p, lo + static_cast<uint32_t>(rb_block) * 64u + lane, rbv);
+
+    if (irregular) {  // L < 44, misaligned, L % 4 != 0, far-apart offsets: per packet
+        for (int b = 0; b < nblocks; ++b) {
+            uint64_t off, boff;
+            uint32_t L;
+            bool reg;
+            uint64_t m = quad_classify(p, lo, nq, b, lane, off, L, reg, boff);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint64_t o = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off), l)) |
+                                   (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off >> 32), l)) << 32);
+                const uint32_t Ll = readlane_u32(L, l);
+                const uint32_t r = quad_slow_packet<MODE>(p, p.base + o, Ll, lds, c, lane);
+                if (lane == 0) store_result<MODE>(p, lo + static_cast<uint32_t>(b) * 64u + static_cast<uint32_t>(l), r);
+            }
+        }
+    }
+}
+
+template <int MODE, int K, int D, bool RAGGED, bool TRAILER>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_quad_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.table_quad);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
+    c.fin = kFinalBase + lane * 4u;
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
+    uint32_t chunk = (p.n + tw - 1) / tw;
+    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 3u) & ~3u;
+    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    if (lo64 >= p.n) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    run_quad<MODE, K, D, RAGGED, TRAILER>(p, lds, c, lane, lo, nq);
+}
+
+}  // namespace
+
+// variant 19: K = 5 rows per chunk, D = 5 chunks in flight; 20: K = 6, D = 4; 21: K = 4, D = 6
+int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool ragged = p.off != nullptr || p.len != nullptr;
+#define ICRC_L(M, K, D, R, T) hipLaunchKernelGGL((icrc_quad_kernel<M, K, D, R, T>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_Q(M, K, D)                                      \
+    do {                                                     \
+        if (ragged) {                                        \
+            if (p.trailer) ICRC_L(M, K, D, true, true);      \
+            else ICRC_L(M, K, D, true, false);               \
+        } else {                                             \
+            if (p.trailer) ICRC_L(M, K, D, false, true);     \
+            else ICRC_L(M, K, D, false, false);              \
+        }                                                    \
+    } while (0)
+#define ICRC_QV(M)                          \
+    do {                                    \
+        if (variant == 19) ICRC_Q(M, 5, 5); \
+        else if (variant == 21) ICRC_Q(M, 4, 6); \
+        else ICRC_Q(M, 6, 4);               \
+    } while (0)
+    if (mode == kCompute) ICRC_QV(kCompute);
+    else ICRC_QV(kVerify);
+#undef ICRC_QV
+#undef ICRC_Q
+#undef ICRC_L
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+}  // namespace icrc

@@ -51,12 +51,13 @@ uint32_t advance_words(uint32_t state, uint32_t nwords) {
     return state;
 }
 
-void build_table_image(uint32_t *img) {
+// Row width W words (64: one packet per wavefront; 16: four packets per wavefront).
+static void build_image(uint32_t *img, uint32_t W) {
     std::memset(img, 0, kLdsBytes);
-    const Matrix m64 = matrix_pow(64);
+    const Matrix mb = matrix_pow(W);
     for (uint32_t b = 0; b < 4; b++) {
         for (uint32_t x = 0; x < 256; x++) {
-            const uint32_t v = m64.apply(x << (8 * b));
+            const uint32_t v = mb.apply(x << (8 * b));
             for (uint32_t copy = 0; copy < 32; copy++) {
                 const uint32_t addr = (b >> 1) * 65536u + x * 256u + (b & 1u) * 128u + copy * 4u;
                 img[addr / 4] = v;
@@ -64,7 +65,7 @@ void build_table_image(uint32_t *img) {
         }
     }
     for (uint32_t lane = 0; lane < 64; lane++) {
-        const Matrix mf = matrix_pow(64u - lane);
+        const Matrix mf = matrix_pow(W - (lane % W));
         for (uint32_t n = 0; n < 8; n++) {
             for (uint32_t v = 0; v < 16; v++) {
                 const uint32_t addr = kFinalBase + (n * 16u + v) * 256u + lane * 4u;
@@ -73,5 +74,9 @@ void build_table_image(uint32_t *img) {
         }
     }
 }
+
+void build_table_image(uint32_t *img) { build_image(img, 64); }
+
+void build_table_image_quad(uint32_t *img) { build_image(img, 16); }
 
 }  // namespace icrc

@@ -150,6 +150,7 @@ def _load() -> ctypes.CDLL:
                                             ctypes.c_uint16, ctypes.c_uint16]),
         "icrc_rdma_header_len": (i32, [ctypes.c_uint8]),
         "icrc_table_image": (i32, [vp, u32]),
+        "icrc_table_image_quad": (i32, [vp, u32]),
         "icrc_write_segment_count": (u32, [u64, u32, u32]),
         "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
         "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
@@ -194,9 +195,11 @@ def version() -> str:
     return lib.icrc_version().decode()
 
 
-def table_image() -> np.ndarray:
+def table_image(quad: bool = False) -> np.ndarray:
+    """The LDS table image the kernels upload (quad=True: the four-packets-per-wavefront one)."""
     img = np.zeros(LDS_WORDS, dtype=np.uint32)
-    _check(lib.icrc_table_image(img.ctypes.data, img.size), "icrc_table_image")
+    fn = lib.icrc_table_image_quad if quad else lib.icrc_table_image
+    _check(fn(img.ctypes.data, img.size), "icrc_table_image")
     return img
 
 

@@ -130,6 +130,67 @@ __global__ __launch_bounds__(1024) void rows_chunk(const uint8_t *base, uint32_t
     }
 }
 
+// E: four packets per wave (16 lanes each, the quad kernel's shape): a group's row is 64 B
+// (one dword per lane), 65 rows per 4156-B packet; chunks of 13 rows double-buffered.
+// X4 = 1: a group's row is 256 B (dwordx4 per lane), 17 rows.
+template <int X4>
+__global__ __launch_bounds__(1024) void quad_rows(const uint8_t *base, uint32_t *out) {
+    const uint32_t lane = threadIdx.x & 63, grp = lane >> 4, col = lane & 15;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave;
+    const uint32_t chunk = ((kN + tw - 1) / tw + 3) & ~3u;
+    const uint32_t lo = gw * chunk;
+    if (lo >= kN) return;
+    const uint32_t nq = kN - lo < chunk ? kN - lo : chunk;
+    auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)lo * kL), 0, (int)(nq * kL), 0x00020000);
+    uint32_t acc = 0;
+    if (X4 == 0) {
+        const int N = 1 + (kL - 4) / 4, R = (N + 15) / 16, k0 = N - 16 * R;  // R = 65
+        constexpr int C = 13;
+        uint32_t ua[C], ub[C];
+        auto load = [&](uint32_t set, int c, uint32_t (&u)[C]) {
+            const uint32_t vb = (set * 4 + grp) * kL + 4u * (uint32_t)(k0 - 1 + (int)col) + 64u * C * c;
+#pragma unroll
+            for (int j = 0; j < C; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 64u * j), 0, 2);
+        };
+        const uint32_t nsets = nq / 4, nch = nsets * 5;
+        load(0, 0, ua);
+        for (uint32_t t = 0; t < nch; t += 2) {
+            if (t + 1 < nch) load((t + 1) / 5, (t + 1) % 5, ub);
+#pragma unroll
+            for (int j = 0; j < C; ++j) acc ^= ua[j];
+            if (t + 1 >= nch) break;
+            if (t + 2 < nch) load((t + 2) / 5, (t + 2) % 5, ua);
+#pragma unroll
+            for (int j = 0; j < C; ++j) acc ^= ub[j];
+        }
+    } else {
+        const int N = 1 + (kL - 4) / 4, R = (N + 63) / 64, k0 = N - 64 * R;  // R = 17
+        uint4 ua[17], ub[17];
+        auto load = [&](uint32_t set, uint4 (&u)[17]) {
+            const uint32_t vb = (set * 4 + grp) * kL + 4u * (uint32_t)(k0 - 1 + 4 * (int)col);
+#pragma unroll
+            for (int j = 0; j < 17; ++j) {
+                auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vb + 256u * j), 0, 2);
+                u[j] = *reinterpret_cast<uint4 *>(&v);
+            }
+        };
+        const uint32_t nsets = nq / 4;
+        load(0, ua);
+        for (uint32_t t = 0; t < nsets; t += 2) {
+            if (t + 1 < nsets) load(t + 1, ub);
+#pragma unroll
+            for (int j = 0; j < 17; ++j) acc ^= ua[j].x ^ ua[j].y ^ ua[j].z ^ ua[j].w;
+            if (t + 1 >= nsets) break;
+            if (t + 2 < nsets) load(t + 2, ua);
+#pragma unroll
+            for (int j = 0; j < 17; ++j) acc ^= ub[j].x ^ ub[j].y ^ ub[j].z ^ ub[j].w;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 template <class F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -184,6 +245,8 @@ int main() {
     RUN_ROWS(rows_chunk, 1, "D chunked dword rows, prefetch 1, per-packet 4-B store")
     RUN_ROWS(rows_chunk, 2, "D chunked dword rows, prefetch 1, coalesced store per 64")
     RUN_ROWS(rows_dword, 1, "B dword rows, 1 pkt/wave in flight, 16 waves/CU (again)")
+    RUN_ROWS(quad_rows, 0, "E quad: 4 pkts/wave, 64-B dword group rows, 13-row chunks x2, nt")
+    RUN_ROWS(quad_rows, 1, "E quad: 4 pkts/wave, 256-B dwordx4 group rows, 17-row sets x2, nt")
     CK(hipFree(d));
     CK(hipFree(out));
     return 0;

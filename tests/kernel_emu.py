@@ -127,3 +127,37 @@ def icrc(img: np.ndarray, pkt: np.ndarray) -> int:
         acc = u if r == 0 else (mul_m64(img, acc) ^ u)
     s = np.bitwise_xor.reduce(final_mul(img, acc))
     return int(~np.uint32(s) & 0xFFFFFFFF)
+
+
+# ---- quad kernel (icrc_quad.hip): four packets per wavefront, 16 lanes per packet ----------
+def _step_lanes(img, s, lanes):
+    lo0 = (lanes & 31) * 4
+    lo1 = lo0 + 128
+    a0 = ((s << 8) & 0xFF00) | lo0
+    a1 = (s & 0xFF00) | lo1
+    a2 = ((s >> 8) & 0xFF00) | (lo0 + 65536)
+    a3 = ((s >> 16) & 0xFF00) | (lo1 + 65536)
+    return _lds(img, a0) ^ _lds(img, a1) ^ _lds(img, a2) ^ _lds(img, a3)
+
+
+def icrc_quad(img16: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0) -> int:
+    """One packet on lanes 16*group .. 16*group+15 of the quad kernel, on the quad table image:
+    end-aligned rows of 16 stream words, `lead` extra leading zero rows (a shorter packet of a
+    set runs behind the set's longest one), acc <- M^16(acc) ^ u, then XOR_c M^(16-c)(acc_c)."""
+    Ld = pkt.size - 4
+    T = 4 + Ld
+    z = (4 - (T & 3)) & 3
+    N = (T + z) >> 2
+    R = (N + 15) >> 4
+    k0 = N - 16 * R
+    lanes = np.arange(16, dtype=np.uint32) + 16 * group
+    col = np.arange(16, dtype=np.int64)
+    acc = np.zeros(16, dtype=np.uint32)
+    for r in range(-lead, R):
+        u = stream_words(pkt, z, k0 + 16 * r + col) if r >= 0 else np.zeros(16, np.uint32)
+        acc = _step_lanes(img16, acc, lanes) ^ u
+    fin = KFINAL + lanes * 4
+    f = np.zeros(16, dtype=np.uint32)
+    for n in range(8):
+        f ^= _lds(img16, fin + n * 4096 + (((acc >> (4 * n)) & 15) << 8))
+    return int(~np.uint32(np.bitwise_xor.reduce(f)) & 0xFFFFFFFF)

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 29, names
+    assert len(names) == 30, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -62,6 +62,26 @@ def test_bad_arguments_rejected_before_device():
     with pytest.raises(icrc_amd.IcrcError) as e:
         icrc_amd.compute_icrc_batch(np.zeros(100, np.uint8), [0], [10])
     assert e.value.rc == icrc_amd.EINVAL
+
+
+def _crc_table():
+    t = []
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ 0xEDB88320 if c & 1 else c >> 1
+        t.append(c)
+    return t
+
+
+_CRC_TABLE = _crc_table()
+
+
+def advance_words(s, n):
+    """M^n(s): the reflected CRC-32 state advanced over 4n zero bytes."""
+    for _ in range(4 * n):
+        s = (s >> 8) ^ _CRC_TABLE[s & 0xFF]
+    return s
 
 
 def test_table_image_against_gf2_definition():
@@ -103,6 +123,39 @@ def test_kernel_algorithm_emulation_matches_oracle(seed):
         assert kernel_emu.icrc(img, p) == oracle.compute_icrc(p), L
     for pkt, want in KATS:
         assert kernel_emu.icrc(img, np.frombuffer(pkt, np.uint8)) == want
+
+
+def test_quad_table_image_layout():
+    """Quad image: M^16 bulk tables, M^(16 - (lane & 15)) final tables, same addressing."""
+    import icrc_amd
+
+    img = icrc_amd.table_image(quad=True)
+    rng = np.random.default_rng(11)
+    for _ in range(64):
+        b, x, copy = int(rng.integers(0, 4)), int(rng.integers(0, 256)), int(rng.integers(0, 32))
+        addr = (b >> 1) * 65536 + x * 256 + (b & 1) * 128 + copy * 4
+        assert img[addr // 4] == advance_words(x << (8 * b), 16)
+    for lane in (0, 1, 15, 16, 31, 47, 63):
+        n, v = int(rng.integers(0, 8)), int(rng.integers(0, 16))
+        addr = 131072 + (n * 16 + v) * 256 + lane * 4
+        assert img[addr // 4] == advance_words(v << (4 * n), 16 - (lane & 15))
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_quad_algorithm_emulation_matches_oracle(seed):
+    """The quad kernel's lane algorithm (any packet group, leading zero rows of a shorter packet
+    in a set) on the product's quad table image, against the oracle."""
+    import icrc_amd
+
+    img = icrc_amd.table_image(quad=True)
+    rng = np.random.default_rng(50 + seed)
+    lengths = [44, 47, 48, 60, 64, 68, 108, 112, 316, 1084, 4156, 4157]
+    for i, L in enumerate(lengths + [int(x) for x in rng.integers(44, 2000, 6)]):
+        p = rng.integers(0, 256, L, dtype=np.uint8)
+        want = oracle.compute_icrc(p)
+        assert kernel_emu.icrc_quad(img, p, group=i % 4, lead=i % 3) == want, L
+    for pkt, want in KATS:
+        assert kernel_emu.icrc_quad(img, np.frombuffer(pkt, np.uint8), group=3, lead=2) == want
 
 
 def test_header_writer_matches_oracle_packet_writer():

@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 16, 17])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 16, 17, 19, 20, 21])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
@@ -109,6 +109,76 @@ def test_every_kernel_variant_is_bit_exact(engine, variant):
         engine.compute_strided(d.data_ptr(), L, L, 777, d_out.data_ptr(), stream=stream_handle())
         torch.cuda.synchronize()
         np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), oracle_icrcs(sbuf, soff, slens))
+    finally:
+        engine.set_variant(-1)
+
+
+def _quad_block_mix(rng, nblocks=48):
+    """Blocks of 64 packets of contrasting shapes for the quad kernel's block / set / bubble
+    logic: tiny 1-row packets (16 sets of 1 row per block: the load side outruns the process
+    side and stalls), blocks with no fast-path packet at all (misaligned), partial sets, one
+    jumbo packet among short ones, unsorted mixed MTUs."""
+    lens, gaps = [], []
+    for b in range(nblocks):
+        kind = b % 6
+        if kind == 0:
+            ln, gp = rng.choice([44, 48, 52, 60, 64], 64), np.zeros(64, int)
+        elif kind == 1:
+            ln, gp = rng.choice([316, 1084], 64), np.ones(64, int)       # misaligned: generic path
+        elif kind == 2:
+            ln, gp = rng.choice([316, 1084, 4156], 64), np.zeros(64, int)
+            gp[rng.integers(0, 64, 5)] = 1                               # a few irregular
+        elif kind == 3:
+            ln, gp = np.full(64, 316), np.zeros(64, int)
+            ln[17] = 9000                                                # jumbo among short
+        elif kind == 4:
+            ln, gp = rng.integers(11, 1100, 64) * 4, np.zeros(64, int)  # every row count
+        else:
+            ln, gp = np.full(64, 4156), np.zeros(64, int)
+        lens.append(ln)
+        gaps.append(gp)
+    lens = np.concatenate(lens).astype(np.uint32)
+    gaps = np.concatenate(gaps).astype(np.uint64)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    return off, lens
+
+
+@pytest.mark.parametrize("variant", [19, 20, 21])
+@pytest.mark.parametrize("n", [3072, 1000, 37])
+def test_quad_block_transitions_compute_verify(engine, variant, n):
+    """Quad kernel on contrasting 64-packet blocks: compute with trailer write, then verify
+    (all ok), then negatives (one flipped bit per 7 packets) with in-place trailer zeroing."""
+    rng = np.random.default_rng(variant * 1000 + n)
+    off, lens = _quad_block_mix(rng)
+    off, lens = off[:n], lens[:n]
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    engine.set_variant(variant)
+    try:
+        out, nerr, wrote = run_batch(engine, buf, off, lens, write_trailer=True)
+        assert nerr == 0
+        want = oracle_icrcs(buf, off, lens)
+        np.testing.assert_array_equal(out, want)
+        for i in range(0, n, 97):
+            t = int(off[i] + lens[i] - 4)
+            assert int(wrote[t: t + 4].view(np.uint32)[0]) == int(want[i])
+        bad = np.arange(0, n, 7)
+        for i in bad:
+            wrote[int(off[i]) + 36 + int(rng.integers(0, int(lens[i]) - 40))] ^= 0x10  # ICRC-covered, unmasked
+        d_buf = dev(wrote)
+        d_off, d_len = dev(off), dev(lens)
+        d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(),
+                            zero_trailer=True, stream=stream_handle())
+        torch.cuda.synchronize()
+        ok = d_ok.cpu().numpy()
+        expect = np.ones(n, np.uint8)
+        expect[bad] = 0
+        np.testing.assert_array_equal(ok, expect)
+        after = d_buf.cpu().numpy()
+        for i in range(0, n, 53):
+            t = int(off[i] + lens[i] - 4)
+            assert not after[t: t + 4].any()
     finally:
         engine.set_variant(-1)
 
