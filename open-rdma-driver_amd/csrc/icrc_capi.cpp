@@ -69,11 +69,27 @@ struct DeviceGuard {
         if ((expr) != hipSuccess) return ICRC_EDEVICE; \
     } while (0)
 
-// Kernel variant of a batch: the engine's forced variant, else the default for its shape (the
-// one-packet-per-wavefront pipeline for uniform strided batches, the quad kernel for ragged).
-int variant_for(const icrc_engine *e, bool ragged) {
-    if (e->variant >= 0) return e->variant;
-    return ragged ? icrc::kDefaultRaggedVariant : icrc::kDefaultVariant;
+int grid_for(const icrc_engine *e, uint32_t n);
+
+// Launch a batch.  A variant forced on the engine runs alone.  Otherwise: a uniform strided
+// batch runs on the one-packet pipeline (variant 13) when its packets are long, on the quad
+// kernel when short; a ragged batch is split by length (hybrid dispatch): the quad kernel takes
+// L < kSplitLen (and every packet off the fast paths), the long-packet kernel the rest.
+int dispatch(const icrc_engine *e, int mode, BatchParams p, void *stream) {
+    const int grid = grid_for(e, p.n);
+    p.split_len = 0;
+    if (e->variant >= 0) {
+        p.variant = e->variant;
+        return icrc::launch_batch(mode, p, grid, stream);
+    }
+    if (p.off == nullptr && p.len == nullptr) {
+        p.variant = p.ulen >= icrc::kSplitLen ? icrc::kDefaultVariant : icrc::kDefaultRaggedVariant;
+        return icrc::launch_batch(mode, p, grid, stream);
+    }
+    p.variant = icrc::kDefaultRaggedVariant;
+    p.split_len = icrc::kSplitLen;
+    const int rc = icrc::launch_batch(mode, p, grid, stream);
+    return rc != ICRC_OK ? rc : icrc::launch_long(mode, p, grid, stream);
 }
 
 int grid_for(const icrc_engine *e, uint32_t n) {
@@ -266,10 +282,9 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
         p.table = e->d_table;
         p.table_quad = e->d_table_quad;
         p.trailer = 0;  // trailers are applied to the caller's host copy in finish_stage
-        p.variant = variant_for(e, true);
         if (mode == icrc::kCompute) p.out = s.d_res;
         else p.ok = reinterpret_cast<uint8_t *>(s.d_res);
-        if ((rc = icrc::launch_batch(mode, p, grid_for(e, cnt), s.stream)) != ICRC_OK) break;
+        if ((rc = dispatch(e, mode, p, s.stream)) != ICRC_OK) break;
         const size_t res_bytes = mode == icrc::kCompute ? cnt * 4 : cnt;
         if (hipMemcpyAsync(s.h_res, s.d_res, res_bytes, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
             hipEventRecord(s.done, s.stream) != hipSuccess) {
@@ -310,8 +325,7 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     p.table = e->d_table;
     p.table_quad = e->d_table_quad;
     p.trailer = trailer ? 1 : 0;
-    p.variant = variant_for(e, d_off != nullptr || d_len != nullptr);
-    return icrc::launch_batch(mode, p, grid_for(e, n), stream);
+    return dispatch(e, mode, p, stream);
 }
 
 }  // namespace

@@ -43,11 +43,16 @@ struct BatchParams {
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
     const uint32_t *table_quad;  // kLdsWords quad image (variants >= kFirstQuadVariant)
+    uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
+                         // long-packet kernel (launch_long) L >= split_len
 };
 
 constexpr int kDefaultVariant = 13;  // S=1, D=1, nt row loads (A/B: profiles/r01_ab_nt.json)
 constexpr int kFirstQuadVariant = 19;  // 19..21: 4 packets per wavefront (chunk pipeline, K x D)
 constexpr int kDefaultRaggedVariant = 20;
+// Hybrid dispatch threshold: shorter packets go to the quad kernel (per-packet costs / 4), longer
+// ones to the one-packet pipeline (one contiguous row per wave instruction streams faster).
+constexpr uint32_t kSplitLen = 2048;
 constexpr int kMaxVariant = 21;
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
@@ -57,6 +62,8 @@ constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
 
 // Launch wrappers (icrc_kernels.hip).  `grid` = number of workgroups.
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
+// One-packet pipeline over the packets with L >= p.split_len of a ragged batch (hybrid dispatch).
+int launch_long(int mode, const BatchParams &p, int grid, void *stream);
 int launch_rx(const BatchParams &p, int grid, void *stream);  // verify + parse (p.rx)
 // Quad kernel (icrc_quad.hip), variant 19..21 (chunk size / chunks in flight).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);

@@ -394,6 +394,124 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     }
 }
 
+// ---- long packets of a ragged batch (hybrid dispatch) ------------------------------------------
+// The one-packet pipeline (S = 1, D-deep prefetch) over only the packets with L >= p.split_len;
+// the quad kernel (icrc_quad.hip) takes the shorter ones, whose per-packet costs it divides by
+// four.  Long packets stay here because one contiguous 256-byte row per wave instruction
+// streams from HBM at ~6.2 TB/s, while four packets per instruction stop at ~4.5 TB/s
+// (profiles/r01_membench.json, patterns D and E).  The walk skips short packets with the
+// ballot of each 64-packet meta block; results are kept per block and stored 64 at a time.
+template <int MODE, int D, int ABL>
+__device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                                   uint32_t lane, uint32_t lo, uint32_t nq) {
+    constexpr int B = D + 1;
+    if (nq == 0) return;
+    MetaBlock mb;
+    mb.block = -1;
+    mb.off_lo = mb.off_hi = mb.len = 0;
+    uint64_t lmask = 0;  // long packets of mb
+    uint32_t qn = 0;     // next candidate (load side)
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    int rb_block = -1;
+    SlotMeta m[B][1];
+    uint32_t qs[B];
+    uint32_t u[B][1][kRows];
+    int inflight = 0;
+
+    auto next = [&](SlotMeta &sm, uint32_t &q) __attribute__((always_inline)) {
+        sm.kind = 0;
+        sm.R = 0;
+        sm.k0 = 0;
+        sm.pkt = p.base;
+        sm.L = 0;
+        q = 0xFFFFFFFFu;
+        while (qn < nq) {
+            const int blk = static_cast<int>(qn >> 6);
+            if (blk != mb.block) {
+                meta_fetch(p, mb, lo, lo + nq, blk, lane);
+                lmask = __ballot(static_cast<uint32_t>(blk) * 64u + lane < nq && mb.len >= p.split_len);
+            }
+            const uint64_t mask = lmask & (~0ull << (qn & 63u));
+            if (mask == 0) {
+                qn = static_cast<uint32_t>(blk + 1) * 64u;
+                continue;
+            }
+            const int l = __builtin_ctzll(mask);
+            q = static_cast<uint32_t>(blk) * 64u + static_cast<uint32_t>(l);
+            qn = q + 1u;
+            const uint64_t off = meta_off(mb, l);
+            const uint32_t L = readlane_u32(mb.len, l);
+            sm.pkt = p.base + off;
+            sm.L = L;
+            sm.kind = 2;
+            if (((reinterpret_cast<uintptr_t>(sm.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+                const int N = 1 + static_cast<int>((L - 4u) >> 2);
+                const int R = (N + 63) >> 6;
+                if (R <= kRows) {
+                    sm.kind = 1;
+                    sm.R = R;
+                    sm.k0 = N - 64 * R;
+                }
+            }
+            return;
+        }
+    };
+
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        next(m[d][0], qs[d]);
+        slot_load<ABL>(m[d][0], lane, u[d][0]);
+        if (m[d][0].kind) inflight += 1;
+    }
+    for (;;) {
+        static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            next(m[bp][0], qs[bp]);
+            slot_load<ABL>(m[bp][0], lane, u[bp][0]);
+            if (m[bp][0].kind) inflight += 1;
+            if (m[b][0].kind) {
+                const int blk = static_cast<int>(qs[b] >> 6);
+                if (blk != rb_block) {
+                    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+                    rb_block = blk;
+                }
+                process_set<MODE, 1, ABL>(p, lds, c, lane, m[b], u[b], qs[b], rb, lo);
+                inflight -= 1;
+            }
+            return true;
+        });
+        if (qn >= nq && inflight == 0) break;
+    }
+    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
+    c.fin = kFinalBase + lane * 4u;
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    if (lo64 >= p.n) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
+}
+
 // ---- row-stream path ------------------------------------------------------------------------
 // A wave's chunk is one flat sequence of 256-byte rows (the sum of R over its regular packets,
 // in packet order).  A ring of RD row loads stays in flight (RD * 256 B per wave); the
@@ -1133,6 +1251,14 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
 }
 #undef ICRC_LAUNCH
 #undef ICRC_QUAD
+
+int launch_long(int mode, const BatchParams &p, int grid, void *stream) {
+    if (grid < 1) grid = 1;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode == kCompute) hipLaunchKernelGGL(icrc_long_kernel<kCompute>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    else hipLaunchKernelGGL(icrc_long_kernel<kVerify>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
 
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;

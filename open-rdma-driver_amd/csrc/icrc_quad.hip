@@ -66,7 +66,8 @@ struct QuadSet {
 // buffer base.  Returns the ballot of the valid packets that are NOT on the fast path.
 __device__ __forceinline__ uint64_t quad_classify_from(const BatchParams &p, uint64_t off, uint32_t L, bool valid,
                                                        uint32_t lo, int b, uint32_t lane, bool &reg, uint64_t &boff) {
-    reg = valid && L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(p.base + off) | L) & 3u) == 0;
+    const bool foreign = valid && p.split_len != 0 && L >= p.split_len;  // the long-packet kernel's
+    reg = valid && !foreign && L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(p.base + off) | L) & 3u) == 0;
     if (p.off == nullptr) {
         boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(b) * 64u) * p.stride;
     } else {  // minimum offset over the fast-path packets (64-bit butterfly)
@@ -82,7 +83,7 @@ __device__ __forceinline__ uint64_t quad_classify_from(const BatchParams &p, uin
                (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(m >> 32), 0)) << 32);
     }
     reg = reg && (off - boff) + L <= kQuadRelLimit;
-    return __ballot(valid && !reg);
+    return __ballot(valid && !reg && !foreign);
 }
 
 // The same, reading (offset, L) from the batch arrays (tail loop).

@@ -144,12 +144,14 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [19, 20, 21])
+@pytest.mark.parametrize("variant", [-1, 19, 20, 21])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
 def test_quad_block_transitions_compute_verify(engine, variant, n):
-    """Quad kernel on contrasting 64-packet blocks: compute with trailer write, then verify
-    (all ok), then negatives (one flipped bit per 7 packets) with in-place trailer zeroing."""
-    rng = np.random.default_rng(variant * 1000 + n)
+    """Quad kernel (19-21) and the default hybrid dispatch (-1: quad for L < 2048, the
+    one-packet pipeline for the rest) on contrasting 64-packet blocks: compute with trailer
+    write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
+    trailer zeroing."""
+    rng = np.random.default_rng((variant + 2) * 1000 + n)
     off, lens = _quad_block_mix(rng)
     off, lens = off[:n], lens[:n]
     buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
