@@ -72,7 +72,8 @@ int icrc_engine_device_ordinal(const icrc_engine *engine);
 void *icrc_engine_stream(const icrc_engine *engine);
 /* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode): 0 = one packet
  * per wavefront at a time, 1..18 = one packet per wavefront, software-pipelined, 19..21 = four
- * packets per wavefront; -1 = the defaults (13 for uniform strided batches, 20 for ragged ones).
+ * packets per wavefront; -1 = the defaults (16 for uniform strided batches of long packets, 20 for
+ * short ones; ragged batches are split by length between 20 and the long-packet kernel).
  * Results are identical. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */

@@ -250,6 +250,15 @@ __device__ __forceinline__ bool static_for(F &&f) {
     }
 }
 
+// Packets per wave (contiguous chunks): whole 64-packet blocks, so that results leave as whole
+// 256-byte lines, unless the batch is too small to give every wave a block — then as few as one
+// packet per wave, so that a small batch (a 16 MiB message: 4096 packets) still spreads over
+// every wave of the grid.
+__device__ __forceinline__ uint32_t wave_chunk(uint32_t n, uint32_t tw) {
+    const uint32_t c = (n + tw - 1) / tw;
+    return c > 32u ? (c + 63u) & ~63u : c;
+}
+
 // v_readlane as an unsigned value (the builtin returns int: widening it directly to 64 bits
 // sign-extends offsets >= 2 GiB).
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {

@@ -47,7 +47,7 @@ struct BatchParams {
                          // long-packet kernel (launch_long) L >= split_len
 };
 
-constexpr int kDefaultVariant = 13;  // S=1, D=1, nt row loads (A/B: profiles/r01_ab_nt.json)
+constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
 constexpr int kFirstQuadVariant = 19;  // 19..21: 4 packets per wavefront (chunk pipeline, K x D)
 constexpr int kDefaultRaggedVariant = 20;
 // Hybrid dispatch threshold: shorter packets go to the quad kernel (per-packet costs / 4), longer

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
     c.fin = kFinalBase + lane * 4u;
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
-    const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+    const uint32_t chunk = wave_chunk(p.n, tw);
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
@@ -743,7 +743,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
     if constexpr (S < 0) {
-        const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+        const uint32_t chunk = wave_chunk(p.n, tw);
         const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
         if (lo64 >= p.n) return;
         const uint32_t lo = static_cast<uint32_t>(lo64);
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
         }
     } else {
         // contiguous chunks, 64-packet aligned so result stores are whole blocks
-        const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+        const uint32_t chunk = wave_chunk(p.n, tw);
         const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
         if (lo64 >= p.n) return;
         const uint32_t lo = static_cast<uint32_t>(lo64);
@@ -785,12 +785,12 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     c.fin = kFinalBase + lane * 4u;
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
-    const uint32_t chunk = ((p.n + tw - 1) / tw + 63u) & ~63u;
+    const uint32_t chunk = wave_chunk(p.n, tw);
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, 1, 1, (kStreamAux << 2) | (DBG ? 3 : 0), true>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, 2, 1, (kStreamAux << 2) | (DBG ? 3 : 0), true>(p, lds, c, lane, lo, nq);
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
@@ -812,12 +812,12 @@ struct SegInfo {
     int R, k0;
 };
 
-struct MsgRegs {  // the 88-byte icrc_write_msg, one dword per lane (lanes 0..21)
-    uint32_t v;
-    int idx;  // uniform: message index held, -1 = none
+struct MsgRegs {  // the 88-byte icrc_write_msg in scalar registers (uniform)
+    uint32_t s[22];
+    int idx;  // message index held, -1 = none
 };
 
-__device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return readlane_u32(m.v, dw); }
+__device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return m.s[dw]; }
 __device__ __forceinline__ uint64_t msg_u64(const MsgRegs &m, int dw) {
     return static_cast<uint64_t>(msg_u32(m, dw)) | (static_cast<uint64_t>(msg_u32(m, dw + 1)) << 32);
 }
@@ -829,17 +829,33 @@ enum : int {
 };
 static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout");
 
+// Message descriptors are read with scalar loads (uniform index, constant address space): they
+// count in lgkmcnt, so fetching one inside the row ring leaves the ring's vmcnt accounting exact
+// (a vector load there made every wait vmcnt(0)).
+using ConstU32 = const __attribute__((address_space(4))) uint32_t;
+
+__device__ __forceinline__ uint32_t msg_first_packet(const icrc_write_msg *msgs, int idx) {
+    return ((ConstU32 *)reinterpret_cast<uintptr_t>(msgs + idx))[16];  // icrc_write_msg::first_packet
+}
+
 __device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t nmsgs, int idx, MsgRegs &m,
                                           uint32_t lane) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(msgs + idx);
-    m.v = (lane < static_cast<uint32_t>(kMsgDwords) && static_cast<uint32_t>(idx) < nmsgs) ? w[lane] : 0u;
+    (void)lane;
     m.idx = idx;
+    if (static_cast<uint32_t>(idx) < nmsgs) {
+        ConstU32 *w = (ConstU32 *)reinterpret_cast<uintptr_t>(msgs + idx);
+#pragma unroll
+        for (int i = 0; i < kMsgDwords; ++i) m.s[i] = w[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kMsgDwords; ++i) m.s[i] = 0u;
+    }
 }
 
 __device__ __forceinline__ void seg_info(const MsgRegs &m, uint32_t s, SegInfo &g) {
     const uint32_t total = msg_u32(m, kMTotal), pmtu = msg_u32(m, kMPmtu);
     const bool by_remote = ((msg_u32(m, kMKind) >> 16) & ICRC_WRITE_SEG_BY_REMOTE_VA) != 0u;
-    const uint32_t lva = static_cast<uint32_t>(msg_u64(m, by_remote ? kMRemoteVa : kMLocalVa));
+    const uint32_t lva = by_remote ? msg_u32(m, kMRemoteVa) : msg_u32(m, kMLocalVa);  // low 32 bits (constant index: m stays in registers)
     uint32_t first = pmtu - lva % pmtu;
     first = total < first ? total : first;
     if (s == 0) {
@@ -941,7 +957,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     c.fin = kFinalBase + lane * 4u;
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
-    const uint32_t chunk = ((npk + tw - 1) / tw + 63u) & ~63u;
+    const uint32_t chunk = wave_chunk(npk, tw);
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= npk) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
@@ -951,7 +967,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     int mlo = 0, mhi = static_cast<int>(nmsgs) - 1;
     while (mlo < mhi) {
         const int mid = (mlo + mhi + 1) >> 1;
-        if (msgs[mid].first_packet <= lo) mlo = mid;
+        if (msg_first_packet(msgs, mid) <= lo) mlo = mid;
         else mhi = mid - 1;
     }
     mlo = __builtin_amdgcn_readfirstlane(mlo);
@@ -1003,7 +1019,6 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
         }
     };
     lc.m.idx = pc.m.idx = -1;
-    lc.m.v = pc.m.v = 0;
     bool slow_seen = false;
     locate(lc, lo);
     if (!lc.fast) advance(lc);
@@ -1100,7 +1115,6 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     if (slow_seen) {
         Cur sc;
         sc.m.idx = -1;
-        sc.m.v = 0;
         for (uint32_t pk = lo; pk < hi; ++pk) {
             locate(sc, pk);
             if (sc.fast) continue;
