@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const L
 __device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uint32_t fin) {
     uint32_t r[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, fin + n * 4096u + (((acc >> (4 * n)) & 15u) << 8));
+    for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, fin + n * 4096u + (__builtin_amdgcn_ubfe(acc, 4 * n, 4) << 8));
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
@@ -76,10 +76,14 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 // prefetched loads of the next packet.)
 __device__ __forceinline__ uint32_t head_mask(int k) {
     const uint32_t kk = static_cast<uint32_t>(k);  // k < 0 wraps large -> 0
-    const uint32_t lo = (0xC000D02Fu >> ((kk & 7u) * 4u)) & 15u;
-    const uint32_t hi = (0x00000010u >> ((kk & 7u) * 4u)) & 15u;
-    const uint32_t nib = kk < 8u ? lo : (kk < 16u ? hi : 0u);
-    return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+    // nibble of word k (k = 0..15) from one 64-bit constant: no select chain (hipcc turned the
+    // two-level select into divergent branches)
+    uint32_t nib = static_cast<uint32_t>(0x00000010C000D02Full >> ((kk & 15u) * 4u)) & 15u;
+    nib = kk < 16u ? nib : 0u;
+    const uint32_t bits = (nib * 0x00204081u) & 0x01010101u;  // bit t -> byte t's low bit
+    // byte selectors 0x0C / 0x0D of v_perm_b32 yield 0x00 / 0xFF (x 0xFF without v_mul_lo_u32,
+    // which a shift-subtract gets folded back into)
+    return __builtin_amdgcn_perm(0u, 0u, 0x0C0C0C0Cu | bits);
 }
 
 __device__ __forceinline__ uint32_t fast_packet_state(const char *lds, const uint8_t *pkt,

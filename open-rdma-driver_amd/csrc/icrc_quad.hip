@@ -293,15 +293,15 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
         }
         const __amdgpu_buffer_rsrc_t lrs =
             __builtin_amdgcn_make_buffer_rsrc(p.base + LB.boff, 0, static_cast<int>(kQuadOOR), 0x00020000);
+        // Row j holds packet word e0 + 16 j of this lane: absent (before the packet, a pad row, an
+        // empty group, no chunk) exactly when that is negative.  One compare + select per row;
+        // the row offset rides in the instruction's immediate field.
+        const int e0 = lhave ? LS.e + 16 * f : kQuadEmptyE;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const int r = f + j;
-            uint32_t vo = kQuadOOR;
-            if (lhave && r >= 0) {
-                vo = vb + 64u * static_cast<uint32_t>(j);
-                if (r < LS.hrows) vo = (LS.e + 16 * r >= 0) ? vo : kQuadOOR;
-            }
-            u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kStreamAux);
+            const uint32_t vo = e0 >= -16 * j ? vb : kQuadOOR;
+            u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo + 64u * static_cast<uint32_t>(j)), 0,
+                                                           kStreamAux);
         }
         if constexpr (MODE == kVerify) {  // lane 16 g: packet g's stored ICRC (the set's last chunk)
             const bool t = lhave && (fl & (1 << 30)) && col == 0u && LS.e != kQuadEmptyE;
@@ -322,11 +322,19 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
         const int fl = cflags[b];
         if (!(fl & (1 << 31))) return;
         const int hr = fl & 0xFF;
-        const int e = static_cast<int>(ce[b]) >> 8;
+        // Stream word k = e + 16 j + 1 of row j; the masked words (k <= 9) span less than one
+        // row, so each lane has at most one: row jh, mask hm, computed once per chunk.
+        int jh = 0;
+        uint32_t hm = 0;
+        if (hr) {
+            const int k0 = (static_cast<int>(ce[b]) >> 8) + 1;
+            jh = k0 >= 0 ? 0 : (15 - k0) >> 4;
+            hm = head_mask(k0 + 16 * jh);
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             uint32_t x = u[b][j];
-            if (j < hr) x |= head_mask(e + 16 * j + 1);
+            if (j < hr) x |= jh == j ? hm : 0u;
             acc = step_m64(lds, acc, x, c);
         }
         inflight -= 1;
