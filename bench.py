@@ -42,8 +42,8 @@ def log(msg: str) -> None:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--pmtu", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
