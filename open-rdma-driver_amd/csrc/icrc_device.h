@@ -20,6 +20,7 @@ struct LaneConsts {
     // byte1 = the same slot + 128 in the odd tables, byte2 = 0x01 (the second 64 KiB region).
     uint32_t pc;
     uint32_t fin;  // per-lane final-table base
+    uint32_t rx_src4, rx_cls, rx_mask;  // receive-parse descriptor layout (rx_lane_init), rx kernel only
 };
 
 // Table addresses of the four state bytes, one v_perm_b32 each: byte b of s lands in
@@ -59,10 +60,10 @@ __device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uin
 // row rotations leave every lane of each 16-lane row holding the row's XOR; the four row
 // values are combined on the scalar unit.  Returns a wave-uniform value.
 __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x124, 0xF, 0xF, false));  // row_ror:4
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true));  // row_ror:4
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true));  // row_ror:8
     return __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 16) ^
            __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
 }

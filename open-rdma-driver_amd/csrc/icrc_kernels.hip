@@ -143,16 +143,45 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) <<
 // (packet_processor.rs:18-71) on the UDP payload with the ICRC stripped; field getters
 // packet.rs:57-98 (BTH), 173-183 (RETH), 222-232 (AETH), 249-251 (Immediate).  Lane k < 18
 // stores dword k of the 72-byte icrc_rx_desc.
+// Per-lane constants of the descriptor layout, set once per kernel (rx_lane_init): descriptor
+// dword `lane` <- header word src (a big-endian field, byte-swapped), kept when its class is
+// present.   dword: 0 va.lo  1 va.hi  2 sec.lo  3 sec.hi  7 rkey  8 dlen  9 sec rkey  10 sec dlen
+//                   11 imm  12 dqpn  13 psn  14 aeth msn   <- header words 11 10 15 14 12 13 16 17
+//                   14 8 9 10.   Classes: 1 RETH, 2 secondary RETH, 4 Imm, 8 AETH, 16 BTH.
+__device__ __forceinline__ void rx_lane_init(LaneConsts &c, uint32_t lane) {
+    uint32_t src = 0, cls = 0;
+    src = lane == 0u ? 11u : src;
+    src = lane == 1u ? 10u : src;
+    src = lane == 2u ? 15u : src;
+    src = lane == 3u ? 14u : src;
+    src = lane == 7u ? 12u : src;
+    src = lane == 8u ? 13u : src;
+    src = lane == 9u ? 16u : src;
+    src = lane == 10u ? 17u : src;
+    src = lane == 11u ? 14u : src;
+    src = lane == 12u ? 8u : src;
+    src = lane == 13u ? 9u : src;
+    src = lane == 14u ? 10u : src;
+    cls = (lane <= 1u || lane == 7u || lane == 8u) ? 1u : cls;
+    cls = (lane == 2u || lane == 3u || lane == 9u || lane == 10u) ? 2u : cls;
+    cls = lane == 11u ? 4u : cls;
+    cls = lane == 14u ? 8u : cls;
+    cls = (lane == 12u || lane == 13u) ? 16u : cls;
+    c.rx_src4 = src << 2;
+    c.rx_cls = cls;
+    c.rx_mask = (lane >= 12u && lane <= 14u) ? 0xFFFFFFu : 0xFFFFFFFFu;
+}
+
+// `hdr` holds packet word w (bytes 4w .. 4w+3, LE, zero past L-4) in lane w for w < 18: the
+// IPv4 + UDP + BTH + up to 32 bytes of extension headers.  Restates to_rdma_message
+// (packet_processor.rs:18-71) on the UDP payload with the ICRC stripped; field getters
+// packet.rs:57-98 (BTH), 173-183 (RETH), 222-232 (AETH), 249-251 (Immediate).  Lane k < 18
+// stores dword k of the 72-byte icrc_rx_desc.  The packet-wide fields are decoded on the
+// scalar unit (three v_readlane), the per-lane ones take one ds_bpermute + v_perm + a class
+// test, and the six computed dwords are selected into their lanes.
 __device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t hdr, uint64_t off, uint32_t L,
-                                         uint32_t icrc_ok, uint32_t lane) {
-    // Packet-wide values, broadcast into every lane with ds_bpermute rather than v_readlane: kept
-    // in VGPRs, they add no scalar-register pressure to the kernel around this epilogue.
-    auto bcast = [&](int w) __attribute__((always_inline)) {
-        return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(w << 2, static_cast<int>(hdr)));
-    };
-    const uint32_t w7 = bcast(7);
-    const uint32_t w9 = bcast(9);
-    const uint32_t w10 = bcast(10);
+                                         uint32_t icrc_ok, uint32_t lane, const LaneConsts &c) {
+    const uint32_t w7 = readlane_u32(hdr, 7), w9 = readlane_u32(hdr, 9), w10 = readlane_u32(hdr, 10);
     const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
     // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
     const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
@@ -166,47 +195,25 @@ __device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t 
                           : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
                                                     : ICRC_RX_OK;
     const bool ack = hs == 16u;
-    uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
-                     (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
-                     (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+    const bool ok = status == ICRC_RX_OK;
+    const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                           (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                           (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
     const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
     const uint64_t poff = off + 28u + hs;
+    // present classes: General metadata has a RETH, Acknowledge an AETH; none on error
+    const uint32_t en = ok ? ((ack ? 8u : 1u) | (hs == 44u ? 2u : 0u) | (hs == 32u ? 4u : 0u) | 16u) : 0u;
 
-    // Per-lane part: dword `lane` of icrc_rx_desc.  Big-endian header fields are gathered from
-    // the header word that holds them (one ds_bpermute) and byte-swapped (one v_perm).
-    //   dword: 0 va.lo  1 va.hi  2 sec.lo  3 sec.hi  7 rkey  8 dlen  9 sec rkey  10 sec dlen
-    //          11 imm  12 dqpn  13 psn  14 aeth msn          <- header words 11 10 15 14 12 13
-    //                                                           16 17 14 8 9 10
-    uint32_t src = 0;
-    src = lane == 0u ? 11u : src;
-    src = lane == 1u ? 10u : src;
-    src = lane == 2u ? 15u : src;
-    src = lane == 3u ? 14u : src;
-    src = lane == 7u ? 12u : src;
-    src = lane == 8u ? 13u : src;
-    src = lane == 9u ? 16u : src;
-    src = lane == 10u ? 17u : src;
-    src = lane == 11u ? 14u : src;
-    src = lane == 12u ? 8u : src;
-    src = lane == 13u ? 9u : src;
-    src = lane == 14u ? 10u : src;
-    const uint32_t g = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src << 2), static_cast<int>(hdr)));
-    uint32_t v = __builtin_amdgcn_perm(g, g, 0x00010203u);  // bswap32
-    const bool reth = !ack;                                  // General metadata: RETH present
-    bool keep = (lane <= 1u || lane == 7u || lane == 8u) ? reth
-              : (lane == 2u || lane == 3u || lane == 9u || lane == 10u) ? hs == 44u
-              : (lane == 11u) ? hs == 32u
-              : (lane == 14u) ? ack
-              : (lane == 12u || lane == 13u);
-    v = keep ? v : 0u;
-    v = (lane >= 12u && lane <= 14u) ? (v & 0xFFFFFFu) : v;
-    v = lane == 4u ? static_cast<uint32_t>(poff) : v;
-    v = lane == 5u ? static_cast<uint32_t>(poff >> 32) : v;
-    v = lane == 6u ? L - 32u - hs - pad : v;
-    v = lane == 15u ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : v;
-    v = lane == 16u ? (flags | (pad << 8) | (code << 16) | (value << 24)) : v;
-    v = status != ICRC_RX_OK ? 0u : v;  // on error every parsed field is 0
-    v = lane == 17u ? ((icrc_ok & 0xFFu) | (status << 8)) : v;
+    const uint32_t g = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c.rx_src4), static_cast<int>(hdr)));
+    uint32_t v = __builtin_amdgcn_perm(g, g, 0x00010203u) & c.rx_mask;  // bswap32
+    v = (c.rx_cls & en) ? v : 0u;
+    auto put = [&](uint32_t x, uint32_t l) __attribute__((always_inline)) { v = lane == l ? x : v; };
+    put(ok ? static_cast<uint32_t>(poff) : 0u, 4);
+    put(ok ? static_cast<uint32_t>(poff >> 32) : 0u, 5);
+    put(ok ? L - 32u - hs - pad : 0u, 6);
+    put(ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u, 15);
+    put(ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u, 16);
+    put((icrc_ok & 0xFFu) | (status << 8), 17);
     if (lane < 18u) reinterpret_cast<uint32_t *>(rx + i)[lane] = v;
 }
 
@@ -322,7 +329,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                     const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
                     rb_put(rb, q0 + s, r);
                     if constexpr (PARSE)
-                        rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane);
+                        rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
                 }
             }
     }
@@ -337,7 +344,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             const uint32_t r = handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane);
             rb_put(rb, q0 + s, r);
             if constexpr (PARSE)
-                rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane);
+                rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
         }
 }
 
@@ -629,7 +636,7 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
                 } else {
                     if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
                     rb_record<MODE>(p, rb, rb_block, lo, cur.q, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN, lane);
-                    if constexpr (PARSE) rx_store(p.rx, lo + cur.q, 0u, off, L, ICRC_VERIFY_BADLEN, lane);
+                    if constexpr (PARSE) rx_store(p.rx, lo + cur.q, 0u, off, L, ICRC_VERIFY_BADLEN, lane, c);
                 }
             }
         }
@@ -682,7 +689,7 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
                 const uint32_t r = packet_result<MODE>(p, pc.pkt, pc.L - 4u, crc, true, lane);
                 rb_record<MODE>(p, rb, rb_block, lo, pc.q, r, lane);
                 if constexpr (PARSE)
-                    rx_store(p.rx, lo + pc.q, hdr, static_cast<uint64_t>(pc.pkt - p.base), pc.L, r, lane);
+                    rx_store(p.rx, lo + pc.q, hdr, static_cast<uint64_t>(pc.pkt - p.base), pc.L, r, lane, c);
                 next_packet(pc, false);
             }
             load_row(ring[i]);
@@ -713,7 +720,7 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
                 if constexpr (PARSE) hdr_slow = rx_header_bytes(pkt, L, lane);  // before the trailer is zeroed
                 const uint32_t r = handle_packet<MODE>(p, pkt, L, lds, c, lane);
                 if (lane == 0) store_result<MODE>(p, lo + q, r);
-                if constexpr (PARSE) rx_store(p.rx, lo + q, hdr_slow, off, L, r, lane);
+                if constexpr (PARSE) rx_store(p.rx, lo + q, hdr_slow, off, L, r, lane, c);
             }
         }
     }
@@ -783,6 +790,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     LaneConsts c;
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
+    rx_lane_init(c, lane);
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
     const uint32_t chunk = wave_chunk(p.n, tw);

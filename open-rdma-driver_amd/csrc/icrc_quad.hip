@@ -37,10 +37,10 @@ __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
 
 // XOR over each 16-lane row (DPP quad_perm x2, row_ror 4, 8): every lane gets its group's XOR.
 __device__ __forceinline__ uint32_t group_xor(uint32_t x) {
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x4E, 0xF, 0xF, false));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x124, 0xF, 0xF, false));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0x128, 0xF, 0xF, false));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0xB1, 0xF, 0xF, true));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x4E, 0xF, 0xF, true));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true));
+    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true));
     return x;
 }
 

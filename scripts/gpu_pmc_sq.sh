@@ -20,7 +20,7 @@ W = os.environ.get("WORKLOAD", "c2")
 for path in sorted(glob.glob(f"gpurun_out/pmcsq_{W}_*/**/*counter_collection.csv", recursive=True)):
     acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
     for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"].split("(")[0][-40:]
+        k = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0].split("::")[-1][:48]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     for k, d in acc.items():
         if "icrc" in k:
