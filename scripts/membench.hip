@@ -191,6 +191,44 @@ __global__ __launch_bounds__(1024) void quad_rows(const uint8_t *base, uint32_t 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// F: the packetizer's copy shape: packet t's payload (4096 B at src + 4096 t) is read in 256-B
+// dword rows and written as a 4156-B wire packet (dst + 4156 t, 4-B aligned) in 256-B dword rows,
+// rows end-aligned like the kernel (row 0 starts 200 B before the packet).  NT = load policy.
+constexpr uint32_t kPay = 4096, kWire = 4156, kCopyN = 786432;
+template <int NT, int STORE_NT>
+__global__ __launch_bounds__(1024) void copy_rows(const uint8_t *src, uint8_t *dst) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave;
+    const uint32_t chunk = ((kCopyN + tw - 1) / tw + 63) & ~63u;
+    const uint32_t lo = gw * chunk;
+    if (lo >= kCopyN) return;
+    const uint32_t nq = kCopyN - lo < chunk ? kCopyN - lo : chunk;
+    constexpr int R = 17;
+    uint32_t ua[R], ub[R];
+    auto load = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)(lo + q) * kPay), 0, (int)kPay, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (lane + 64u * j) - 256u), 0, NT ? 2 : 0);
+    };
+    auto store = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)(lo + q) * kWire), 0, (int)(kWire - 4), 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            __builtin_amdgcn_raw_buffer_store_b32(u[j], rs, (int)(4u * (lane + 64u * j) - 200u), 0, STORE_NT ? 2 : 0);
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        store(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        store(q + 1, ub);
+    }
+}
+
 template <class F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -247,6 +285,20 @@ int main() {
     RUN_ROWS(rows_dword, 1, "B dword rows, 1 pkt/wave in flight, 16 waves/CU (again)")
     RUN_ROWS(quad_rows, 0, "E quad: 4 pkts/wave, 64-B dword group rows, 13-row chunks x2, nt")
     RUN_ROWS(quad_rows, 1, "E quad: 4 pkts/wave, 256-B dwordx4 group rows, 17-row sets x2, nt")
+    {
+        uint8_t *wire;
+        CK(hipMalloc(&wire, (size_t)kCopyN * kWire + 4096));
+        auto copy_report = [&](const char *name, float ms) {
+            const double b = (double)kCopyN * (kPay + kWire);
+            printf("{\"pattern\": \"%s\", \"ms\": %.4f, \"GB/s (read+write)\": %.1f}\n", name, ms, b / (ms * 1e-3) / 1e9);
+            fflush(stdout);
+        };
+        copy_report("F copy 4096-B payload -> 4156-B wire packets, 256-B dword rows, default",
+                    time_it([&] { copy_rows<0, 0><<<cus, 1024>>>(d, wire); }, reps));
+        copy_report("F copy ..., nt loads", time_it([&] { copy_rows<1, 0><<<cus, 1024>>>(d, wire); }, reps));
+        copy_report("F copy ..., nt loads + nt stores", time_it([&] { copy_rows<1, 1><<<cus, 1024>>>(d, wire); }, reps));
+        CK(hipFree(wire));
+    }
     CK(hipFree(d));
     CK(hipFree(out));
     return 0;
