@@ -200,6 +200,7 @@ def main() -> int:
                       f"(oracle/icrc_fast.c); matches GPU: {cpu_ok}",
         }
         result["parity_sample_ok"] = cpu_ok
+        result["cpu_context"] = cpu_context(orc, host, L, cs, args.cpu_seconds / 4)
 
     if args.extra:
         result["extra"] = extra_measurements(eng, stream, args, world)
@@ -210,6 +211,25 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0 if parity else 1
+
+
+def cpu_context(orc, host, L, cs, budget):
+    """Beside the 1-core cpu_baseline: the same port on every core of this job's CPU
+    share (the box caps a job at 16; os.cpu_count() reports the whole machine), and the emulator's
+    per-packet send path around compute_icrc on one core (8 KiB vec alloc + memset, payload copy
+    in, CRC, UDP-payload copy out: net/util.rs:172-186, packet_processor.rs:210-265)."""
+    threads = max(1, min(16, os.cpu_count() or 1))
+    out = {}
+    for name, fn in (("all_cores", lambda: orc.fast_icrc_strided_timed(host, L, L, cs, threads=threads)),
+                     ("emulator_path_1_core", lambda: orc.fast_emulator_path_timed(host, L, L, cs))):
+        secs, passes = 0.0, 0
+        while secs < budget or passes == 0:
+            s, _ = fn()
+            secs += s
+            passes += 1
+        out[name] = {"GiB/s": round(cs * L * passes / secs / GIB, 3),
+                     "cores": threads if name == "all_cores" else 1, "seconds": round(secs, 2)}
+    return out
 
 
 def extra_measurements(eng, stream, args, world):
