@@ -30,6 +30,10 @@ constexpr uint32_t kQuadOOR = 0x80000000u;        // voffset past the range: the
 constexpr uint32_t kQuadRelLimit = 0x7F000000u;   // packet offset in its block + L stay below
 constexpr uint32_t kQuadIrregular = 0x3FFFFFFu;   // sort key (>> 6) of a non-fast-path slot
 constexpr int kQuadEmptyE = -(1 << 30);          // word index of a group with no packet
+// Row loads use the default cache policy: a 128-byte line here is read by two or more load
+// instructions (64 bytes per packet group each), and non-temporal loads re-fetch it every time:
+// four packets per wave read 3.7 TB/s with nt, 6.2 TB/s without (profiles/r01_membench_policy.json).
+constexpr int kQuadAux = 0;
 
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
@@ -301,12 +305,12 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
         for (int j = 0; j < K; ++j) {
             const uint32_t vo = e0 >= -16 * j ? vb : kQuadOOR;
             u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo + 64u * static_cast<uint32_t>(j)), 0,
-                                                           kStreamAux);
+                                                           kQuadAux);
         }
         if constexpr (MODE == kVerify) {  // lane 16 g: packet g's stored ICRC (the set's last chunk)
             const bool t = lhave && (fl & (1 << 30)) && col == 0u && LS.e != kQuadEmptyE;
             const uint32_t vo = t ? LS.vb + 64u * static_cast<uint32_t>(LS.rows) : kQuadOOR;
-            u[b][K] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kStreamAux);
+            u[b][K] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kQuadAux);
         }
         cflags[b] = fl;
         if (lhave) {

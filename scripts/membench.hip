@@ -191,6 +191,43 @@ __global__ __launch_bounds__(1024) void quad_rows(const uint8_t *base, uint32_t 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// G: P packets per wave (64/P lanes each, dword rows of 256/P bytes per packet), the packets
+// of a set adjacent in memory; chunks of 16 rows double-buffered.  P = 2, 4, 8.
+template <int P, int AUX = 2>
+__global__ __launch_bounds__(1024) void multi_rows(const uint8_t *base, uint32_t *out) {
+    constexpr int W = 64 / P;  // lanes (words) per packet row
+    const uint32_t lane = threadIdx.x & 63, grp = lane / W, col = lane % W;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave;
+    const uint32_t chunk = ((kN + tw - 1) / tw + P - 1) / P * P;
+    const uint32_t lo = gw * chunk;
+    if (lo >= kN) return;
+    const uint32_t nq = kN - lo < chunk ? kN - lo : chunk;
+    auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)lo * kL), 0, (int)(nq * kL), 0x00020000);
+    const int N = 1 + (kL - 4) / 4, R = (N + W - 1) / W, k0 = N - W * R;
+    constexpr int C = 16;
+    const int nch = (R + C - 1) / C;
+    uint32_t acc = 0, ua[C], ub[C];
+    auto load = [&](uint32_t set, int ch, uint32_t (&u)[C]) {
+        const uint32_t vb = (set * P + grp) * kL + 4u * (uint32_t)(k0 - 1 + (int)col) + 4u * W * C * ch;
+#pragma unroll
+        for (int j = 0; j < C; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 4u * W * j), 0, AUX);
+    };
+    const uint32_t nsets = nq / P, total = nsets * nch;
+    load(0, 0, ua);
+    for (uint32_t t = 0; t < total; t += 2) {
+        if (t + 1 < total) load((t + 1) / nch, (t + 1) % nch, ub);
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc ^= ua[j];
+        if (t + 1 >= total) break;
+        if (t + 2 < total) load((t + 2) / nch, (t + 2) % nch, ua);
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc ^= ub[j];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // F: the packetizer's copy shape: packet t's payload (4096 B at src + 4096 t) is read in 256-B
 // dword rows and written as a 4156-B wire packet (dst + 4156 t, 4-B aligned) in 256-B dword rows,
 // rows end-aligned like the kernel (row 0 starts 200 B before the packet).  NT = load policy.
@@ -285,6 +322,21 @@ int main() {
     RUN_ROWS(rows_dword, 1, "B dword rows, 1 pkt/wave in flight, 16 waves/CU (again)")
     RUN_ROWS(quad_rows, 0, "E quad: 4 pkts/wave, 64-B dword group rows, 13-row chunks x2, nt")
     RUN_ROWS(quad_rows, 1, "E quad: 4 pkts/wave, 256-B dwordx4 group rows, 17-row sets x2, nt")
+    RUN_ROWS(multi_rows, 2, "G 2 pkts/wave, 128-B dword rows per packet, 16-row chunks x2, nt")
+    RUN_ROWS(multi_rows, 4, "G 4 pkts/wave, 64-B dword rows per packet, 16-row chunks x2, nt")
+    RUN_ROWS(multi_rows, 8, "G 8 pkts/wave, 32-B dword rows per packet, 16-row chunks x2, nt")
+    {
+        float ms = time_it([&] { multi_rows<2, 0><<<cus, 1024>>>(d, out); }, reps);
+        report("G 2 pkts/wave, default policy", ms);
+        ms = time_it([&] { multi_rows<4, 0><<<cus, 1024>>>(d, out); }, reps);
+        report("G 4 pkts/wave, default policy", ms);
+        ms = time_it([&] { multi_rows<4, 1><<<cus, 1024>>>(d, out); }, reps);
+        report("G 4 pkts/wave, glc (sc0)", ms);
+        ms = time_it([&] { multi_rows<1, 2><<<cus, 1024>>>(d, out); }, reps);
+        report("G 1 pkt/wave (same code), nt", ms);
+        ms = time_it([&] { multi_rows<1, 0><<<cus, 1024>>>(d, out); }, reps);
+        report("G 1 pkt/wave (same code), default", ms);
+    }
     {
         uint8_t *wire;
         CK(hipMalloc(&wire, (size_t)kCopyN * kWire + 4096));
