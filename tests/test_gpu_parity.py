@@ -701,3 +701,56 @@ def test_ragged_offsets_beyond_2GiB(engine):
     assert np.all(desc["payload_offset"][ok_parse] >= np.asarray(off)[ok_parse] + 28)
     del d_buf
     torch.cuda.empty_cache()
+
+
+def test_empty_batches_are_noops(engine):
+    """n == 0 on every device entry point: OK, nothing written (the reference's loops simply do
+    not run on an empty packet list)."""
+    import icrc_amd
+
+    guard = torch.full((64,), 0x5A, dtype=torch.uint8, device="cuda")
+    p = guard.data_ptr()
+    s = stream_handle()
+    engine.compute_batch(p, p, p, 0, p, write_trailer=True, stream=s)
+    engine.verify_batch(p, p, p, 0, p, zero_trailer=True, stream=s)
+    engine.compute_strided(p, 64, 64, 0, p, True, s)
+    engine.verify_strided(p, 64, 64, 0, p, True, s)
+    engine.rx_parse(p, 0, 0, 0, p, p, stride=64, length=64, stream=s)
+    engine.ipv4_checksum(p, 0, stride=64, d_csum=p, fill=True, stream=s)
+    torch.cuda.synchronize()
+    assert bool((guard == 0x5A).all().item())
+    assert icrc_amd.compute_icrc_batch(np.zeros(0, np.uint8), [], []).size == 0
+
+
+@pytest.mark.parametrize("pmtu", [256, 1024])
+def test_short_strided_stream_quad_path(engine, pmtu):
+    """Uniform strided batches of short packets go to the quad kernel (non-ragged variant):
+    compute, trailer write and verify against the oracle."""
+    n = 2000 + pmtu // 256  # not a multiple of 4 or 64
+    buf, off, lens = oracle.synth_middle_stream(n, pmtu=pmtu)
+    L = int(lens[0])
+    d = dev(buf)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.compute_strided(d.data_ptr(), L, L, n, d_out.data_ptr(), True, stream_handle())
+    torch.cuda.synchronize()
+    want = oracle_icrcs(buf, off, lens)
+    np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), want)
+    host = d.cpu().numpy()
+    np.testing.assert_array_equal(host.reshape(n, L)[:, L - 4:].copy().view(np.uint32).ravel(), want)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_strided(d.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream_handle())
+    torch.cuda.synchronize()
+    assert bool((d_ok == 1).all().item())
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5])
+def test_tiny_batches_every_path(engine, n):
+    """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block."""
+    rng = np.random.default_rng(900 + n)
+    lens = rng.choice([44, 316, 1084, 4156, 9000], n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
+    out, nerr, _ = run_batch(engine, buf, off, lens)
+    assert nerr == 0
+    np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
