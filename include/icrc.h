@@ -72,8 +72,10 @@ int icrc_engine_device_ordinal(const icrc_engine *engine);
 void *icrc_engine_stream(const icrc_engine *engine);
 /* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode): 0 = one packet
  * per wavefront at a time, 1..18 = one packet per wavefront, software-pipelined, 19..21 = four
- * packets per wavefront; -1 = the defaults (16 for uniform strided batches of long packets, 20 for
- * short ones; ragged batches are split by length between 20 and the long-packet kernel).
+ * packets per wavefront, 24..30 = eight packets per wavefront, 100 + q (q in 19..30) = the
+ * default length-split dispatch with q as its short-packet kernel; -1 = the defaults (16 for
+ * uniform strided batches of long packets, 24 for short ones; ragged batches are split by length
+ * between 24 and the long-packet kernel).
  * Results are identical. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
@@ -298,6 +300,8 @@ int icrc_table_image(uint32_t *out_words, uint32_t nwords);
 /* The quad kernel's image (four packets per wavefront): M^16 bulk tables, M^(16 - (l & 15))
  * final tables, same layout. */
 int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords);
+/* The oct kernel's image (eight packets per wavefront): M^8 bulk, M^(8 - (l & 7)) final. */
+int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords);
 
 #ifdef __cplusplus
 }

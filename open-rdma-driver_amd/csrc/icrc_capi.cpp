@@ -42,6 +42,7 @@ struct icrc_engine {
     int variant = -1;  // -1: kDefaultVariant for strided batches, kDefaultRaggedVariant otherwise
     uint32_t *d_table = nullptr;
     uint32_t *d_table_quad = nullptr;
+    uint32_t *d_table_oct = nullptr;
     hipStream_t stream = nullptr;
     std::mutex mu;  // guards the host-batch stages
     Stage st[2];
@@ -78,15 +79,16 @@ int grid_for(const icrc_engine *e, uint32_t n);
 int dispatch(const icrc_engine *e, int mode, BatchParams p, void *stream) {
     const int grid = grid_for(e, p.n);
     p.split_len = 0;
-    if (e->variant >= 0) {
+    if (e->variant >= 0 && e->variant < icrc::kHybridVariantBase) {
         p.variant = e->variant;
         return icrc::launch_batch(mode, p, grid, stream);
     }
+    const int short_variant = e->variant < 0 ? icrc::kDefaultRaggedVariant : e->variant - icrc::kHybridVariantBase;
     if (p.off == nullptr && p.len == nullptr) {
-        p.variant = p.ulen >= icrc::kSplitLen ? icrc::kDefaultVariant : icrc::kDefaultRaggedVariant;
+        p.variant = p.ulen >= icrc::kSplitLen ? icrc::kDefaultVariant : short_variant;
         return icrc::launch_batch(mode, p, grid, stream);
     }
-    p.variant = icrc::kDefaultRaggedVariant;
+    p.variant = short_variant;
     p.split_len = icrc::kSplitLen;
     const int rc = icrc::launch_batch(mode, p, grid, stream);
     return rc != ICRC_OK ? rc : icrc::launch_long(mode, p, grid, stream);
@@ -281,6 +283,7 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
         p.n = cnt;
         p.table = e->d_table;
         p.table_quad = e->d_table_quad;
+        p.table_oct = e->d_table_oct;
         p.trailer = 0;  // trailers are applied to the caller's host copy in finish_stage
         if (mode == icrc::kCompute) p.out = s.d_res;
         else p.ok = reinterpret_cast<uint8_t *>(s.d_res);
@@ -324,6 +327,7 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     p.nerr = d_nerr;
     p.table = e->d_table;
     p.table_quad = e->d_table_quad;
+    p.table_oct = e->d_table_oct;
     p.trailer = trailer ? 1 : 0;
     return dispatch(e, mode, p, stream);
 }
@@ -363,13 +367,16 @@ int icrc_engine_create(int device, icrc_engine **out) {
         return ICRC_EDEVICE;
     }
     e->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
-    std::vector<uint32_t> img(icrc::kLdsWords), img_quad(icrc::kLdsWords);
+    std::vector<uint32_t> img(icrc::kLdsWords), img_quad(icrc::kLdsWords), img_oct(icrc::kLdsWords);
     icrc::build_table_image(img.data());
     icrc::build_table_image_quad(img_quad.data());
+    icrc::build_table_image_oct(img_oct.data());
     if (hipMalloc(&e->d_table, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table, img.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_table_quad, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&e->d_table_oct, icrc::kLdsBytes) != hipSuccess ||
+        hipMemcpy(e->d_table_oct, img_oct.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         icrc_engine_destroy(e);
         return ICRC_EDEVICE;
@@ -386,6 +393,7 @@ int icrc_engine_destroy(icrc_engine *e) {
         for (Stage &s : e->st) stage_free(s);
         if (e->d_table) (void)hipFree(e->d_table);
         if (e->d_table_quad) (void)hipFree(e->d_table_quad);
+        if (e->d_table_oct) (void)hipFree(e->d_table_oct);
         if (e->stream) (void)hipStreamDestroy(e->stream);
     }
     {
@@ -423,7 +431,9 @@ int icrc_engine_default(int device, icrc_engine **out) {
 int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : ICRC_EINVAL; }
 
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
-    if (!e || variant < -1 || variant > icrc::kMaxVariant) return ICRC_EINVAL;
+    const bool hybrid = variant >= icrc::kHybridVariantBase + icrc::kFirstQuadVariant &&
+                        variant <= icrc::kHybridVariantBase + icrc::kMaxVariant;
+    if (!e || variant < -1 || (variant > icrc::kMaxVariant && !hybrid)) return ICRC_EINVAL;
     e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;
 }
@@ -608,6 +618,12 @@ int icrc_table_image(uint32_t *out_words, uint32_t nwords) {
 int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image_quad(out_words);
+    return ICRC_OK;
+}
+
+int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords) {
+    if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
+    icrc::build_table_image_oct(out_words);
     return ICRC_OK;
 }
 

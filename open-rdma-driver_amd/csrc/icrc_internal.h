@@ -24,6 +24,8 @@ void build_table_image(uint32_t *img);
 // final tables — so the final lookup of lane l = 16 g + c is conflict-free across the 4
 // packet groups g (bank (16 g + c) of each 256-byte table row).
 void build_table_image_quad(uint32_t *img);
+// Oct image (eight packets per wavefront, 8 lanes each): M^8 bulk, M^(8 - (l & 7)) final.
+void build_table_image_oct(uint32_t *img);
 // Host reference helpers used by the table builder (exposed for unit tests).
 uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
 
@@ -42,18 +44,21 @@ struct BatchParams {
     int trailer;     // compute: write trailer; verify: zero trailer
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
-    const uint32_t *table_quad;  // kLdsWords quad image (variants >= kFirstQuadVariant)
+    const uint32_t *table_quad;  // kLdsWords quad image (W = 16: variants 19-23)
+    const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 24-30)
     uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
                          // long-packet kernel (launch_long) L >= split_len
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
 constexpr int kFirstQuadVariant = 19;  // 19..21: 4 packets per wavefront (chunk pipeline, K x D)
-constexpr int kDefaultRaggedVariant = 20;
+constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
 // Hybrid dispatch threshold: shorter packets go to the quad kernel (per-packet costs / 4), longer
 // ones to the one-packet pipeline (one contiguous row per wave instruction streams faster).
 constexpr uint32_t kSplitLen = 2048;
-constexpr int kMaxVariant = 21;
+// 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
+constexpr int kHybridVariantBase = 100;
+constexpr int kMaxVariant = 35;  // 22, 23, 31, 32: quad / oct ablations (wrong results by design); 24-30: oct
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

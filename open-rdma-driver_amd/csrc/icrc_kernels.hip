@@ -123,7 +123,7 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
         return;
     }
     constexpr int kAux = abl_aux(ABL);
-    const int nrec = (abl_mode(ABL) != 3 && m.kind == 1) ? static_cast<int>(m.L - 4u) : 0;  // mode 3: no access
+    const int nrec = m.kind == 1 ? static_cast<int>(m.L - 4u) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
     const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
     // Always kRows loads, no branch: hipcc's static vmcnt accounting takes the minimum over
@@ -230,18 +230,6 @@ __device__ __forceinline__ uint32_t rx_header_bytes(const uint8_t *pkt, uint32_t
     return w;
 }
 
-// Diagnostic (ABL mode 3): dword 0 = packet index, 4/5 = offset, 6 = length, 17 = kind.
-__device__ __forceinline__ void rx_debug_store(icrc_rx_desc *rx, uint32_t i, int64_t off, uint32_t L, uint32_t kind,
-                                               uint32_t lane) {
-    uint32_t v = 0;
-    v = lane == 0u ? i : v;
-    v = lane == 4u ? static_cast<uint32_t>(off) : v;
-    v = lane == 5u ? static_cast<uint32_t>(static_cast<uint64_t>(off) >> 32) : v;
-    v = lane == 6u ? L : v;
-    v = lane == 17u ? kind : v;
-    if (lane < 18u) reinterpret_cast<uint32_t *>(rx + i)[lane] = v;
-}
-
 // PARSE: gather packet words 0..17 into lanes 0..17 from the first two rows as loaded (raw, before
 // the ICRC masks): word w sits in row j, lane w + 1 - k0 - 64 j.
 __device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row1, int k0, uint32_t lane) {
@@ -322,23 +310,15 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 #pragma unroll
         for (int s = 0; s < S; ++s)
             if (m[s].kind == 1) {
-                if constexpr (abl_mode(ABL) == 3) {  // diagnostic: record the packet's (offset, len) only
-                    rb_put(rb, q0 + s, 0u);
-                    if constexpr (PARSE) rx_debug_store(p.rx, lo + q0 + s, m[s].pkt - p.base, m[s].L, 1u, lane);
-                } else {
-                    const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
-                    rb_put(rb, q0 + s, r);
-                    if constexpr (PARSE)
-                        rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
-                }
+                const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
+                rb_put(rb, q0 + s, r);
+                if constexpr (PARSE)
+                    rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
             }
     }
 #pragma unroll
     for (int s = 0; s < S; ++s)
-        if (abl_mode(ABL) == 3 && m[s].kind == 2) {
-            rb_put(rb, q0 + s, 0u);
-            if constexpr (PARSE) rx_debug_store(p.rx, lo + q0 + s, m[s].pkt - p.base, m[s].L, 2u, lane);
-        } else if (m[s].kind == 2) {
+        if (m[s].kind == 2) {
             uint32_t hdr_slow = 0;
             if constexpr (PARSE) hdr_slow = rx_header_bytes(m[s].pkt, m[s].L, lane);  // before any trailer zeroing
             const uint32_t r = handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane);
@@ -776,7 +756,6 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 
 // Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
 // words gathered from each packet's first two rows.
-template <int DBG>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -798,7 +777,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, 2, 1, (kStreamAux << 2) | (DBG ? 3 : 0), true>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, 2, 1, kStreamAux << 2, true>(p, lds, c, lane, lo, nq);
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
@@ -1282,7 +1261,21 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2)); break;  // diagnostic: CRC only (same code shape as 15)
     case 19:  // four packets per wave (icrc_quad.hip): K rows per chunk, D chunks in flight
     case 20:
-    case 21: ICRC_QUAD(p.variant); break;
+    case 21:
+    case 22:  // diagnostic: quad kernel, loads only
+    case 23:  // diagnostic: quad kernel, no loads
+    case 24:  // eight packets per wave (W = 8)
+    case 25:
+    case 26:
+    case 27:
+    case 28:
+    case 29:
+    case 30:
+    case 31:
+    case 32:
+    case 33:
+    case 34:
+    case 35: ICRC_QUAD(p.variant); break;
     default: ICRC_LAUNCH(1, 2, 0); break;
     }
 }
@@ -1317,11 +1310,7 @@ int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr,
 int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
-    static const bool dbg = getenv("ICRC_RX_DEBUG") != nullptr;  // diagnostic: meta walk only
-    if (dbg)
-        hipLaunchKernelGGL((icrc_rx_kernel<1>), dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
-    else
-        hipLaunchKernelGGL((icrc_rx_kernel<0>), dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(icrc_rx_kernel, dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

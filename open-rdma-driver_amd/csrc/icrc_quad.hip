@@ -39,14 +39,30 @@ __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
 }
 
-// XOR over each 16-lane row (DPP quad_perm x2, row_ror 4, 8): every lane gets its group's XOR.
+// XOR over each W-lane packet group (DPP quad_perm x2, then row_ror 4, 8 for W = 16 or
+// row_half_mirror for W = 8): every lane gets its group's XOR.
+template <int W>
 __device__ __forceinline__ uint32_t group_xor(uint32_t x) {
     x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0xB1, 0xF, 0xF, true));
     x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x4E, 0xF, 0xF, true));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true));
+    if constexpr (W == 16) {
+        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true));
+        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true));
+    } else {
+        static_assert(W == 8, "packet groups of 8 or 16 lanes");
+        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x141, 0xF, 0xF, true));
+    }
     return x;
 }
+
+// Geometry of a W-lane packet group: G = 64 / W packets per wavefront.
+template <int W>
+struct Geo {
+    static constexpr int G = 64 / W;
+    static constexpr int LW = W == 16 ? 4 : 3;
+    static constexpr int LG = W == 16 ? 2 : 3;
+    static constexpr int HR = 1 + (9 + W - 1) / W;  // packet rows that can hold masked header words
+};
 
 struct QuadBlock {
     uint32_t key;   // per lane p (sorted position): R << 6 | block index of the packet
@@ -108,12 +124,14 @@ __device__ __forceinline__ uint64_t quad_classify(const BatchParams &p, uint32_t
 
 // Block b: classification, then the fast-path packets sorted by row count (bitonic sort of
 // R << 6 | index across the lanes; skipped when already sorted).
+template <int W>
 __device__ __forceinline__ void quad_block_from(const BatchParams &p, QuadBlock &B, uint64_t off, uint32_t L,
                                                 bool valid, uint32_t lo, int b, uint32_t lane, bool &irregular) {
+    using Gm = Geo<W>;
     uint64_t boff;
     bool reg;
     if (quad_classify_from(p, off, L, valid, lo, b, lane, reg, boff) != 0) irregular = true;
-    const uint32_t R = reg ? (1u + ((L - 4u) >> 2) + 15u) >> 4 : kQuadIrregular;
+    const uint32_t R = reg ? (1u + ((L - 4u) >> 2) + (W - 1u)) >> Gm::LW : kQuadIrregular;
     uint32_t key = (R << 6) | lane;
     const uint32_t nxt = bperm((lane + 1u) & 63u, key);
     if (__ballot(lane == 63u || key <= nxt) != ~0ull) {
@@ -138,31 +156,34 @@ __device__ __forceinline__ void quad_block_from(const BatchParams &p, QuadBlock 
     B.regmask = __ballot(reg);
     B.boff = boff;
     B.block = b;
-    B.nsets = (__popcll(B.regmask) + 3) >> 2;
+    B.nsets = (__popcll(B.regmask) + Gm::G - 1) >> Gm::LG;
 }
 
+template <int W>
 __device__ __forceinline__ void quad_set(const QuadBlock &B, int s, uint32_t lane, QuadSet &S) {
+    using Gm = Geo<W>;
+    constexpr int G = Gm::G;
     const int nreg = __popcll(B.regmask);
-    const uint32_t ps = static_cast<uint32_t>(4 * s) + (lane >> 4);
+    const uint32_t ps = static_cast<uint32_t>(G * s) + (lane >> Gm::LW);
     const uint32_t key = bperm(ps & 63u, B.key);
     const uint32_t vrel = bperm(ps & 63u, B.vrel);
     const uint32_t L = bperm(ps & 63u, B.len);
-    const int last = (4 * s + 3 < nreg) ? 4 * s + 3 : nreg - 1;
+    const int last = (G * s + G - 1 < nreg) ? G * s + G - 1 : nreg - 1;
     const int Rmax = static_cast<int>(readlane_u32(B.key, last) >> 6);
-    const int Rmin = static_cast<int>(readlane_u32(B.key, 4 * s) >> 6);
+    const int Rmin = static_cast<int>(readlane_u32(B.key, G * s) >> 6);
     const int R = static_cast<int>(key >> 6);
     const int N = 1 + static_cast<int>((L - 4u) >> 2);
-    const int k0 = N - 16 * R;
+    const int k0 = N - W * R;
     const bool valid = static_cast<int>(ps) < nreg;
-    S.e = valid ? k0 - 1 + static_cast<int>(lane & 15u) - 16 * (Rmax - R) : kQuadEmptyE;
+    S.e = valid ? k0 - 1 + static_cast<int>(lane & (W - 1u)) - W * (Rmax - R) : kQuadEmptyE;
     S.vb = vrel + 4u * static_cast<uint32_t>(S.e);
     S.rows = Rmax;
-    const int full = 4 * s + 3 < nreg;
-    S.hrows = full ? (Rmax - Rmin + 2 < Rmax ? Rmax - Rmin + 2 : Rmax) : Rmax + 1;
+    const int full = G * s + G - 1 < nreg;
+    S.hrows = full ? (Rmax - Rmin + Gm::HR < Rmax ? Rmax - Rmin + Gm::HR : Rmax) : Rmax + 1;
 }
 
-// Generic per-packet path on the quad tables (group 0 computes; wave-uniform result).
-template <int MODE>
+// Generic per-packet path on the W-lane tables (group 0 computes; wave-uniform result).
+template <int MODE, int W>
 __device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
                                                      const LaneConsts &c, uint32_t lane) {
     if (L < ICRC_MIN_PACKET) {
@@ -174,14 +195,14 @@ __device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8
     const uint32_t T = 4u + Ld;
     const int z = static_cast<int>((4u - (T & 3u)) & 3u);
     const int N = static_cast<int>((T + static_cast<uint32_t>(z)) >> 2);
-    const int R = (N + 15) >> 4;
-    const int k0 = N - 16 * R;
-    const int col = static_cast<int>(lane & 15u);
-    const bool g0 = lane < 16u;
+    const int R = (N + W - 1) / W;
+    const int k0 = N - W * R;
+    const int col = static_cast<int>(lane & (W - 1u));
+    const bool g0 = lane < static_cast<uint32_t>(W);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pkt, 0, aligned ? static_cast<int>(Ld) : 0, 0x00020000);
     uint32_t acc = 0;
     for (int r = 0; r < R; ++r) {
-        const int k = k0 + 16 * r + col;
+        const int k = k0 + W * r + col;
         uint32_t u;
         if (aligned) {
             u = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(4u * static_cast<uint32_t>(k - 1)), 0, 0);
@@ -192,7 +213,7 @@ __device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8
         u = g0 ? u : 0u;
         acc = step_m64(lds, acc, u, c);
     }
-    const uint32_t crc = ~readlane_u32(group_xor(final_mul(lds, acc, c.fin)), 0);
+    const uint32_t crc = ~readlane_u32(group_xor<W>(final_mul(lds, acc, c.fin)), 0);
     return packet_result<MODE>(p, pkt, Ld, crc, aligned, lane);
 }
 
@@ -206,15 +227,17 @@ __device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8
 // a ragged batch's next-block (offset, len) is loaded once per ring cycle, unconditionally:
 // the compiler's vmcnt accounting stays exact and no wait drains the ring.
 
-template <int MODE, int K, int D, bool RAGGED, bool TRAILER>
+template <int W, int MODE, int K, int D, bool RAGGED, bool TRAILER, int ABLATE = 0>
 __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                          uint32_t lo, uint32_t nq) {
+    using Gm = Geo<W>;
+    constexpr uint32_t RB = 4u * W;  // bytes per packet row
     constexpr int B = D + 1;
     constexpr int KT = MODE == kVerify ? K + 1 : K;  // verify: + the stored trailers
     if (nq == 0) return;
     const int nblocks = static_cast<int>((nq + 63u) >> 6);
-    const uint32_t grp = lane >> 4;
-    const uint32_t col = lane & 15u;
+    const uint32_t grp = lane >> Gm::LW;
+    const uint32_t col = lane & (W - 1u);
     bool irregular = false;
 
     // Next block NB, prepared at the top of a ring cycle (one copy of the sort, not B), from
@@ -272,7 +295,7 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
                 ldone = true;
             }  // else a stall: the next block is prepared at the top of the next cycle
             if (ok) {
-                quad_set(LB, lset, lane, LS);
+                quad_set<W>(LB, lset, lane, LS);
                 f = LS.rows - ((LS.rows + K - 1) / K) * K;
                 lhave = true;
             }
@@ -280,36 +303,41 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
         int fl = 0;
         uint32_t vb = 0;
         if (lhave) {
-            vb = LS.vb + 64u * static_cast<uint32_t>(f);
-            const int hr = LS.hrows - f;
-            fl = (1 << 31) | (hr < 0 ? 0 : (hr > K ? K : hr));
+            vb = LS.vb + RB * static_cast<uint32_t>(f);
+            // chunk rows [js, je) may hold header words: set rows [0, hrows) sit at chunk rows - f
+            const int js = f < 0 ? -f : 0;
+            int je = LS.hrows - f;
+            je = je > K ? K : je;
+            fl = (1 << 31) | (je > js ? (js << 8) | je : 0);
             const bool last = f + K >= LS.rows;
             if (last) fl |= 1 << 30;
             const uint32_t ps = LB.pos;
-            const bool mine = last && ((LB.regmask >> lane) & 1ull) && static_cast<int>(ps >> 2) == lset;
-            const int e = LS.e + 16 * f;
-            ce[b] = (static_cast<uint32_t>(e < -(1 << 20) ? -(1 << 20) : e) << 8) | (mine ? (ps & 3u) << 4 : 0xFFu);
+            const bool mine = last && ((LB.regmask >> lane) & 1ull) && static_cast<int>(ps >> Gm::LG) == lset;
+            const int e = LS.e + W * f;
+            ce[b] = (static_cast<uint32_t>(e < -(1 << 20) ? -(1 << 20) : e) << 8) |
+                    (mine ? (ps & (Gm::G - 1u)) << Gm::LW : 0xFFu);
             if constexpr (TRAILER) {
-                ctr[b] = (col == 0u && LS.e != kQuadEmptyE) ? LS.vb + 64u * static_cast<uint32_t>(LS.rows) : kQuadOOR;
+                ctr[b] = (col == 0u && LS.e != kQuadEmptyE) ? LS.vb + RB * static_cast<uint32_t>(LS.rows) : kQuadOOR;
             }
             cblk[b] = lblk;
             cboff[b] = LB.boff;
         }
         const __amdgpu_buffer_rsrc_t lrs =
             __builtin_amdgcn_make_buffer_rsrc(p.base + LB.boff, 0, static_cast<int>(kQuadOOR), 0x00020000);
-        // Row j holds packet word e0 + 16 j of this lane: absent (before the packet, a pad row, an
-        // empty group, no chunk) exactly when that is negative.  One compare + select per row;
-        // the row offset rides in the instruction's immediate field.
-        const int e0 = lhave ? LS.e + 16 * f : kQuadEmptyE;
+        // Row j holds packet word e0 + W j of this lane: absent (before the packet, a pad row, an
+        // empty group, no chunk) exactly when that is negative.  One compare + select per row.
+        const int e0 = lhave ? LS.e + W * f : kQuadEmptyE;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint32_t vo = e0 >= -16 * j ? vb : kQuadOOR;
-            u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo + 64u * static_cast<uint32_t>(j)), 0,
-                                                           kQuadAux);
+            const uint32_t vo = e0 >= -W * j ? vb : kQuadOOR;
+            if constexpr (ABLATE >= 2) u[b][j] = vo ^ static_cast<uint32_t>(j);  // diagnostic: no loads
+            else
+                u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo + RB * static_cast<uint32_t>(j)), 0,
+                                                               kQuadAux);
         }
-        if constexpr (MODE == kVerify) {  // lane 16 g: packet g's stored ICRC (the set's last chunk)
+        if constexpr (MODE == kVerify) {  // lane W g: packet g's stored ICRC (the set's last chunk)
             const bool t = lhave && (fl & (1 << 30)) && col == 0u && LS.e != kQuadEmptyE;
-            const uint32_t vo = t ? LS.vb + 64u * static_cast<uint32_t>(LS.rows) : kQuadOOR;
+            const uint32_t vo = t ? LS.vb + RB * static_cast<uint32_t>(LS.rows) : kQuadOOR;
             u[b][K] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo), 0, kQuadAux);
         }
         cflags[b] = fl;
@@ -325,29 +353,45 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
         constexpr int b = decltype(bc)::value;
         const int fl = cflags[b];
         if (!(fl & (1 << 31))) return;
-        const int hr = fl & 0xFF;
-        // Stream word k = e + 16 j + 1 of row j; the masked words (k <= 9) span less than one
-        // row, so each lane has at most one: row jh, mask hm, computed once per chunk.
-        int jh = 0;
-        uint32_t hm = 0;
-        if (hr) {
+        const int js = (fl >> 8) & 0xFF, je = fl & 0xFF;
+        // Stream word k = e + W j + 1 of row j; the masked words (k <= 9) are W apart in a
+        // column, so a lane has at most one (W = 16) or two (W = 8): rows jh, jh + 1, masks
+        // hm, hm2.  They lie in chunk rows [js, je) (uniform); in a set of equal row counts that
+        // window is at most HR rows, masked by one of K fixed-row sequences (a uniform branch on
+        // js), and the other rows cost nothing; wider windows mask every row.
+        if (je > js) {
             const int k0 = (static_cast<int>(ce[b]) >> 8) + 1;
-            jh = k0 >= 0 ? 0 : (15 - k0) >> 4;
-            hm = head_mask(k0 + 16 * jh);
+            const int jh = k0 >= 0 ? 0 : (W - 1 - k0) >> Gm::LW;
+            const uint32_t hm = head_mask(k0 + W * jh);
+            const uint32_t hm2 = W < 16 ? head_mask(k0 + W * (jh + 1)) : 0u;
+            if (je - js <= Gm::HR) {
+#pragma unroll
+                for (int c0 = 0; c0 < K; ++c0) {
+                    if (js == c0) {
+#pragma unroll
+                        for (int r = 0; r < Gm::HR; ++r) {
+                            const int j = c0 + r;
+                            if (j < K) u[b][j] |= (jh == j ? hm : 0u) | (W < 16 && jh + 1 == j ? hm2 : 0u);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < K; ++j) u[b][j] |= (jh == j ? hm : 0u) | (W < 16 && jh + 1 == j ? hm2 : 0u);
+            }
         }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            uint32_t x = u[b][j];
-            if (j < hr) x |= jh == j ? hm : 0u;
-            acc = step_m64(lds, acc, x, c);
+            if constexpr (ABLATE == 1 || ABLATE == 3) acc ^= u[b][j];  // diagnostic: loads only / overhead only
+            else acc = step_m64(lds, acc, u[b][j], c);
         }
         inflight -= 1;
         if (fl & (1 << 30)) {
-            const uint32_t crc = ~group_xor(final_mul(lds, acc, c.fin));
+            const uint32_t crc = ~group_xor<W>(final_mul(lds, acc, c.fin));
             acc = 0;
             uint32_t r;
             if constexpr (MODE == kCompute) r = crc;
-            else r = bperm(grp << 4, u[b][K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+            else r = bperm(grp << Gm::LW, u[b][K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
             if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(p.base + cboff[b], 0, static_cast<int>(kQuadOOR), 0x00020000);
@@ -379,7 +423,7 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
                             : static_cast<uint64_t>(lo + q) * p.stride;
                 L = p.len ? m_len : p.ulen;
             }
-            quad_block_from(p, NB, off, L, valid, lo, nb_next, lane, irregular);
+            quad_block_from<W>(p, NB, off, L, valid, lo, nb_next, lane, irregular);
             nb_next += 1;
             nb_ready = NB.nsets > 0;
         }
@@ -417,19 +461,19 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
                 const uint64_t o = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off), l)) |
                                    (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off >> 32), l)) << 32);
                 const uint32_t Ll = readlane_u32(L, l);
-                const uint32_t r = quad_slow_packet<MODE>(p, p.base + o, Ll, lds, c, lane);
+                const uint32_t r = quad_slow_packet<MODE, W>(p, p.base + o, Ll, lds, c, lane);
                 if (lane == 0) store_result<MODE>(p, lo + static_cast<uint32_t>(b) * 64u + static_cast<uint32_t>(l), r);
             }
         }
     }
 }
 
-template <int MODE, int K, int D, bool RAGGED, bool TRAILER>
-__global__ __launch_bounds__(kThreadsPerGroup) void icrc_quad_kernel(BatchParams p) {
+template <int W, int MODE, int K, int D, bool RAGGED, bool TRAILER, int ABLATE = 0, int NT = kThreadsPerGroup>
+__global__ __launch_bounds__(NT) void icrc_quad_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.table_quad);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+        const uint4 *src = reinterpret_cast<const uint4 *>(W == 16 ? p.table_quad : p.table_oct);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += NT) lds4[i] = src[i];
     }
     __syncthreads();
     const char *lds = reinterpret_cast<const char *>(lds4);
@@ -438,45 +482,74 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_quad_kernel(BatchParams
     LaneConsts c;
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
-    const uint32_t tw = gridDim.x * kWavesPerGroup;
-    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t tw = gridDim.x * (NT / 64);
+    const uint32_t gw = blockIdx.x * (NT / 64) + wave;
     // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
     uint32_t chunk = (p.n + tw - 1) / tw;
-    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 3u) & ~3u;
+    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + (64u / W - 1u)) & ~(64u / W - 1u);
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_quad<MODE, K, D, RAGGED, TRAILER>(p, lds, c, lane, lo, nq);
+    run_quad<W, MODE, K, D, RAGGED, TRAILER, ABLATE>(p, lds, c, lane, lo, nq);
 }
 
 }  // namespace
 
-// variant 19: K = 5 rows per chunk, D = 5 chunks in flight; 20: K = 6, D = 4; 21: K = 4, D = 6
+// Quad (W = 16): variant 19: K = 5 rows per chunk, D = 5 chunks in flight; 20: K = 6, D = 4;
+// 21: K = 4, D = 6; 22 / 23: ablations of 20 (loads only / no loads, compute, ragged).
+// Oct (W = 8): 24: K = 10, D = 3; 25: K = 8, D = 4; 26: K = 5, D = 6; 27: K = 12, D = 3;
+// 28: K = 10, D = 4; 29: K = 17, D = 2; 30: K = 7, D = 5; 31 / 32: ablations of 24 (as 22 / 23).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool ragged = p.off != nullptr || p.len != nullptr;
-#define ICRC_L(M, K, D, R, T) hipLaunchKernelGGL((icrc_quad_kernel<M, K, D, R, T>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
-#define ICRC_Q(M, K, D)                                      \
-    do {                                                     \
-        if (ragged) {                                        \
-            if (p.trailer) ICRC_L(M, K, D, true, true);      \
-            else ICRC_L(M, K, D, true, false);               \
-        } else {                                             \
-            if (p.trailer) ICRC_L(M, K, D, false, true);     \
-            else ICRC_L(M, K, D, false, false);              \
-        }                                                    \
+#define ICRC_L(W, M, K, D, R, T, ...) \
+    hipLaunchKernelGGL((icrc_quad_kernel<W, M, K, D, R, T, ##__VA_ARGS__>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_L512(W, M, K, D, R, T, A) \
+    hipLaunchKernelGGL((icrc_quad_kernel<W, M, K, D, R, T, A, 512>), dim3(grid), dim3(512), 0, s, p)
+#define ICRC_Q(W, M, K, D)                                      \
+    do {                                                        \
+        if (ragged) {                                           \
+            if (p.trailer) ICRC_L(W, M, K, D, true, true);      \
+            else ICRC_L(W, M, K, D, true, false);               \
+        } else {                                                \
+            if (p.trailer) ICRC_L(W, M, K, D, false, true);     \
+            else ICRC_L(W, M, K, D, false, false);              \
+        }                                                       \
     } while (0)
-#define ICRC_QV(M)                          \
-    do {                                    \
-        if (variant == 19) ICRC_Q(M, 5, 5); \
-        else if (variant == 21) ICRC_Q(M, 4, 6); \
-        else ICRC_Q(M, 6, 4);               \
+#define ICRC_QV(M)                                  \
+    do {                                            \
+        switch (variant) {                          \
+        case 19: ICRC_Q(16, M, 5, 5); break;        \
+        case 21: ICRC_Q(16, M, 4, 6); break;        \
+        case 24: ICRC_Q(8, M, 10, 3); break;        \
+        case 25: ICRC_Q(8, M, 8, 4); break;         \
+        case 26: ICRC_Q(8, M, 5, 6); break;         \
+        case 27: ICRC_Q(8, M, 12, 3); break;        \
+        case 28: ICRC_Q(8, M, 10, 4); break;        \
+        case 29: ICRC_Q(8, M, 17, 2); break;        \
+        case 30: ICRC_Q(8, M, 7, 5); break;         \
+        default: ICRC_Q(16, M, 6, 4); break;        \
+        }                                           \
     } while (0)
+    if (variant == 33 || variant == 34) {  // diagnostic: 8 waves per CU (occupancy probe)
+        if (variant == 33) ICRC_L512(8, kCompute, 10, 3, true, false, 0);
+        else ICRC_L512(8, kCompute, 10, 3, true, false, 2);
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
+    if (variant == 22 || variant == 23 || variant == 31 || variant == 32 || variant == 35) {
+        if (variant == 22) ICRC_L(16, kCompute, 6, 4, true, false, 1);
+        else if (variant == 23) ICRC_L(16, kCompute, 6, 4, true, false, 2);
+        else if (variant == 31) ICRC_L(8, kCompute, 10, 3, true, false, 1);
+        else if (variant == 32) ICRC_L(8, kCompute, 10, 3, true, false, 2);
+        else ICRC_L(8, kCompute, 10, 3, true, false, 3);
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
     if (mode == kCompute) ICRC_QV(kCompute);
     else ICRC_QV(kVerify);
 #undef ICRC_QV
 #undef ICRC_Q
+#undef ICRC_L512
 #undef ICRC_L
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }

@@ -79,4 +79,6 @@ void build_table_image(uint32_t *img) { build_image(img, 64); }
 
 void build_table_image_quad(uint32_t *img) { build_image(img, 16); }
 
+void build_table_image_oct(uint32_t *img) { build_image(img, 8); }
+
 }  // namespace icrc

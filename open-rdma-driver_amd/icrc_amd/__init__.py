@@ -151,6 +151,7 @@ def _load() -> ctypes.CDLL:
         "icrc_rdma_header_len": (i32, [ctypes.c_uint8]),
         "icrc_table_image": (i32, [vp, u32]),
         "icrc_table_image_quad": (i32, [vp, u32]),
+        "icrc_table_image_oct": (i32, [vp, u32]),
         "icrc_write_segment_count": (u32, [u64, u32, u32]),
         "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
         "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
@@ -195,10 +196,11 @@ def version() -> str:
     return lib.icrc_version().decode()
 
 
-def table_image(quad: bool = False) -> np.ndarray:
-    """The LDS table image the kernels upload (quad=True: the four-packets-per-wavefront one)."""
+def table_image(width: int = 64) -> np.ndarray:
+    """The LDS table image the kernels upload for rows of `width` words: 64 (one packet per
+    wavefront), 16 (quad: four packets per wavefront) or 8 (oct: eight)."""
     img = np.zeros(LDS_WORDS, dtype=np.uint32)
-    fn = lib.icrc_table_image_quad if quad else lib.icrc_table_image
+    fn = {64: lib.icrc_table_image, 16: lib.icrc_table_image_quad, 8: lib.icrc_table_image_oct}[width]
     _check(fn(img.ctypes.data, img.size), "icrc_table_image")
     return img
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one workload a few times with the default dispatch (for rocprofv3 --pmc / --stats).
 
-usage: run_workload.py {c1,c2,c3} [launches] [variant]"""
+usage: run_workload.py {c1,c2,c3,s316} [launches] [variant]   (s316: 4 Mi strided 316-byte packets)"""
 import os
 import sys
 
@@ -22,8 +22,8 @@ def main():
     if len(sys.argv) > 3:
         eng.set_variant(int(sys.argv[3]))
     s = torch.cuda.current_stream().cuda_stream
-    if which == "c1":
-        w = workloads.write_middle_stream(1 << 20)
+    if which in ("c1", "s316"):
+        w = workloads.write_middle_stream(1 << 20) if which == "c1" else workloads.write_middle_stream(1 << 22, pmtu=256)
         L = int(w.lens[0])
         b = workloads.synthesize(eng, w, stream=s)
         out = torch.zeros(w.n, dtype=torch.int32, device="cuda")

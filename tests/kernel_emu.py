@@ -140,24 +140,25 @@ def _step_lanes(img, s, lanes):
     return _lds(img, a0) ^ _lds(img, a1) ^ _lds(img, a2) ^ _lds(img, a3)
 
 
-def icrc_quad(img16: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0) -> int:
-    """One packet on lanes 16*group .. 16*group+15 of the quad kernel, on the quad table image:
-    end-aligned rows of 16 stream words, `lead` extra leading zero rows (a shorter packet of a
-    set runs behind the set's longest one), acc <- M^16(acc) ^ u, then XOR_c M^(16-c)(acc_c)."""
+def icrc_quad(img: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0, W: int = 16) -> int:
+    """One packet on lanes W*group .. W*group+W-1 of the quad (W = 16) or oct (W = 8) kernel, on
+    that kernel's table image: end-aligned rows of W stream words, `lead` extra leading zero
+    rows (a shorter packet of a set runs behind the set's longest one), acc <- M^W(acc) ^ u,
+    then XOR_c M^(W-c)(acc_c)."""
     Ld = pkt.size - 4
     T = 4 + Ld
     z = (4 - (T & 3)) & 3
     N = (T + z) >> 2
-    R = (N + 15) >> 4
-    k0 = N - 16 * R
-    lanes = np.arange(16, dtype=np.uint32) + 16 * group
-    col = np.arange(16, dtype=np.int64)
-    acc = np.zeros(16, dtype=np.uint32)
+    R = (N + W - 1) // W
+    k0 = N - W * R
+    lanes = np.arange(W, dtype=np.uint32) + W * group
+    col = np.arange(W, dtype=np.int64)
+    acc = np.zeros(W, dtype=np.uint32)
     for r in range(-lead, R):
-        u = stream_words(pkt, z, k0 + 16 * r + col) if r >= 0 else np.zeros(16, np.uint32)
-        acc = _step_lanes(img16, acc, lanes) ^ u
+        u = stream_words(pkt, z, k0 + W * r + col) if r >= 0 else np.zeros(W, np.uint32)
+        acc = _step_lanes(img, acc, lanes) ^ u
     fin = KFINAL + lanes * 4
-    f = np.zeros(16, dtype=np.uint32)
+    f = np.zeros(W, dtype=np.uint32)
     for n in range(8):
-        f ^= _lds(img16, fin + n * 4096 + (((acc >> (4 * n)) & 15) << 8))
+        f ^= _lds(img, fin + n * 4096 + (((acc >> (4 * n)) & 15) << 8))
     return int(~np.uint32(np.bitwise_xor.reduce(f)) & 0xFFFFFFFF)

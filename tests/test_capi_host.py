@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 30, names
+    assert len(names) == 31, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -125,37 +125,40 @@ def test_kernel_algorithm_emulation_matches_oracle(seed):
         assert kernel_emu.icrc(img, np.frombuffer(pkt, np.uint8)) == want
 
 
-def test_quad_table_image_layout():
-    """Quad image: M^16 bulk tables, M^(16 - (lane & 15)) final tables, same addressing."""
+@pytest.mark.parametrize("W", [16, 8])
+def test_quad_table_image_layout(W):
+    """Quad / oct images: M^W bulk tables, M^(W - (lane % W)) final tables, same addressing."""
     import icrc_amd
 
-    img = icrc_amd.table_image(quad=True)
-    rng = np.random.default_rng(11)
+    img = icrc_amd.table_image(width=W)
+    rng = np.random.default_rng(11 + W)
     for _ in range(64):
         b, x, copy = int(rng.integers(0, 4)), int(rng.integers(0, 256)), int(rng.integers(0, 32))
         addr = (b >> 1) * 65536 + x * 256 + (b & 1) * 128 + copy * 4
-        assert img[addr // 4] == advance_words(x << (8 * b), 16)
-    for lane in (0, 1, 15, 16, 31, 47, 63):
+        assert img[addr // 4] == advance_words(x << (8 * b), W)
+    for lane in (0, 1, 7, 8, 15, 16, 31, 47, 63):
         n, v = int(rng.integers(0, 8)), int(rng.integers(0, 16))
         addr = 131072 + (n * 16 + v) * 256 + lane * 4
-        assert img[addr // 4] == advance_words(v << (4 * n), 16 - (lane & 15))
+        assert img[addr // 4] == advance_words(v << (4 * n), W - (lane % W))
 
 
+@pytest.mark.parametrize("W", [16, 8])
 @pytest.mark.parametrize("seed", range(2))
-def test_quad_algorithm_emulation_matches_oracle(seed):
-    """The quad kernel's lane algorithm (any packet group, leading zero rows of a shorter packet
-    in a set) on the product's quad table image, against the oracle."""
+def test_quad_algorithm_emulation_matches_oracle(seed, W):
+    """The quad / oct kernels' lane algorithm (any packet group, leading zero rows of a shorter
+    packet in a set) on the product's table image, against the oracle."""
     import icrc_amd
 
-    img = icrc_amd.table_image(quad=True)
+    img = icrc_amd.table_image(width=W)
+    G = 64 // W
     rng = np.random.default_rng(50 + seed)
-    lengths = [44, 47, 48, 60, 64, 68, 108, 112, 316, 1084, 4156, 4157]
+    lengths = [44, 47, 48, 60, 64, 68, 76, 80, 108, 112, 316, 1084, 4156, 4157]
     for i, L in enumerate(lengths + [int(x) for x in rng.integers(44, 2000, 6)]):
         p = rng.integers(0, 256, L, dtype=np.uint8)
         want = oracle.compute_icrc(p)
-        assert kernel_emu.icrc_quad(img, p, group=i % 4, lead=i % 3) == want, L
+        assert kernel_emu.icrc_quad(img, p, group=i % G, lead=i % 3, W=W) == want, L
     for pkt, want in KATS:
-        assert kernel_emu.icrc_quad(img, np.frombuffer(pkt, np.uint8), group=3, lead=2) == want
+        assert kernel_emu.icrc_quad(img, np.frombuffer(pkt, np.uint8), group=G - 1, lead=2, W=W) == want
 
 
 def test_header_writer_matches_oracle_packet_writer():

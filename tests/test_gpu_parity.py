@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 16, 17, 19, 20, 21])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 16, 17, 19, 20, 21, 24, 25, 26])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
@@ -144,14 +144,14 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [-1, 19, 20, 21])
+@pytest.mark.parametrize("variant", [-1, 19, 20, 21, 24, 25, 26, 120])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
 def test_quad_block_transitions_compute_verify(engine, variant, n):
-    """Quad kernel (19-21) and the default hybrid dispatch (-1: quad for L < 2048, the
-    one-packet pipeline for the rest) on contrasting 64-packet blocks: compute with trailer
+    """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
+    one-packet pipeline for the rest; 120: the same with quad) on contrasting 64-packet blocks: compute with trailer
     write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
     trailer zeroing."""
-    rng = np.random.default_rng((variant + 2) * 1000 + n)
+    rng = np.random.default_rng((variant % 100 + 2) * 1000 + n)
     off, lens = _quad_block_mix(rng)
     off, lens = off[:n], lens[:n]
     buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
@@ -722,24 +722,33 @@ def test_empty_batches_are_noops(engine):
     assert icrc_amd.compute_icrc_batch(np.zeros(0, np.uint8), [], []).size == 0
 
 
+@pytest.mark.parametrize("variant", [-1, 120])
 @pytest.mark.parametrize("pmtu", [256, 1024])
-def test_short_strided_stream_quad_path(engine, pmtu):
-    """Uniform strided batches of short packets go to the quad kernel (non-ragged variant):
-    compute, trailer write and verify against the oracle."""
+def test_short_strided_stream_quad_path(engine, pmtu, variant):
+    """Uniform strided batches of short packets go to the oct (-1) or quad (120) kernel
+    (non-ragged variant): compute, trailer write and verify against the oracle."""
     n = 2000 + pmtu // 256  # not a multiple of 4 or 64
     buf, off, lens = oracle.synth_middle_stream(n, pmtu=pmtu)
     L = int(lens[0])
     d = dev(buf)
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
-    engine.compute_strided(d.data_ptr(), L, L, n, d_out.data_ptr(), True, stream_handle())
-    torch.cuda.synchronize()
+    engine.set_variant(variant)
+    try:
+        engine.compute_strided(d.data_ptr(), L, L, n, d_out.data_ptr(), True, stream_handle())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_variant(-1)
     want = oracle_icrcs(buf, off, lens)
     np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), want)
     host = d.cpu().numpy()
     np.testing.assert_array_equal(host.reshape(n, L)[:, L - 4:].copy().view(np.uint32).ravel(), want)
     d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    engine.verify_strided(d.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream_handle())
-    torch.cuda.synchronize()
+    engine.set_variant(variant)
+    try:
+        engine.verify_strided(d.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream_handle())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_variant(-1)
     assert bool((d_ok == 1).all().item())
 
 
