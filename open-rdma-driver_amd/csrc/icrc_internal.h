@@ -45,7 +45,7 @@ struct BatchParams {
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
     const uint32_t *table_quad;  // kLdsWords quad image (W = 16: variants 19-23)
-    const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 24-30)
+    const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 24-35)
     uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
                          // long-packet kernel (launch_long) L >= split_len
 };
@@ -58,7 +58,7 @@ constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
 constexpr uint32_t kSplitLen = 2048;
 // 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
 constexpr int kHybridVariantBase = 100;
-constexpr int kMaxVariant = 35;  // 22, 23, 31, 32: quad / oct ablations (wrong results by design); 24-30: oct
+constexpr int kMaxVariant = 38;  // 22, 23, 31-38: quad / oct ablations and probes (wrong results by design)
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 

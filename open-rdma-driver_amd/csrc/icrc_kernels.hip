@@ -1275,7 +1275,10 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 32:
     case 33:
     case 34:
-    case 35: ICRC_QUAD(p.variant); break;
+    case 35:
+    case 36:
+    case 37:
+    case 38: ICRC_QUAD(p.variant); break;
     default: ICRC_LAUNCH(1, 2, 0); break;
     }
 }

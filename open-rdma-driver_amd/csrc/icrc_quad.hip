@@ -330,7 +330,7 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t vo = e0 >= -W * j ? vb : kQuadOOR;
-            if constexpr (ABLATE >= 2) u[b][j] = vo ^ static_cast<uint32_t>(j);  // diagnostic: no loads
+            if constexpr (ABLATE >= 2) u[b][j] = vo ^ static_cast<uint32_t>(j);  // diagnostic: no loads (2..5)
             else
                 u[b][j] = __builtin_amdgcn_raw_buffer_load_b32(lrs, static_cast<int>(vo + RB * static_cast<uint32_t>(j)), 0,
                                                                kQuadAux);
@@ -349,65 +349,81 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
     };
 
     // process side of one ring position: buffer b
-    auto p_consume = [&](auto bc) __attribute__((always_inline)) {
+    // process side: header masks of buffer b (stream word k = e + W j + 1 of row j; the masked
+    // words k <= 9 are W apart in a column, so a lane has at most one (W = 16) or two (W = 8):
+    // rows jh, jh + 1, masks hm, hm2.  They lie in chunk rows [js, je) (uniform).  When a set
+    // of equal row counts starts the chunk (js = 0: no pad rows, e.g. 316-byte packets in
+    // chunks of 10 rows) that is rows 0 .. HR - 1, and the other rows cost nothing; any other
+    // window masks every row.)
+    auto p_masks = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
         const int fl = cflags[b];
-        if (!(fl & (1 << 31))) return;
         const int js = (fl >> 8) & 0xFF, je = fl & 0xFF;
-        // Stream word k = e + W j + 1 of row j; the masked words (k <= 9) are W apart in a
-        // column, so a lane has at most one (W = 16) or two (W = 8): rows jh, jh + 1, masks
-        // hm, hm2.  They lie in chunk rows [js, je) (uniform); in a set of equal row counts that
-        // window is at most HR rows, masked by one of K fixed-row sequences (a uniform branch on
-        // js), and the other rows cost nothing; wider windows mask every row.
         if (je > js) {
             const int k0 = (static_cast<int>(ce[b]) >> 8) + 1;
             const int jh = k0 >= 0 ? 0 : (W - 1 - k0) >> Gm::LW;
             const uint32_t hm = head_mask(k0 + W * jh);
             const uint32_t hm2 = W < 16 ? head_mask(k0 + W * (jh + 1)) : 0u;
-            if (je - js <= Gm::HR) {
+            if (js == 0 && je <= Gm::HR) {  // the set starts the chunk: rows 0 .. HR - 1
 #pragma unroll
-                for (int c0 = 0; c0 < K; ++c0) {
-                    if (js == c0) {
-#pragma unroll
-                        for (int r = 0; r < Gm::HR; ++r) {
-                            const int j = c0 + r;
-                            if (j < K) u[b][j] |= (jh == j ? hm : 0u) | (W < 16 && jh + 1 == j ? hm2 : 0u);
-                        }
-                    }
-                }
+                for (int j = 0; j < (Gm::HR < K ? Gm::HR : K); ++j)
+                    u[b][j] |= (jh == j ? hm : 0u) | (W < 16 && jh + 1 == j ? hm2 : 0u);
             } else {
 #pragma unroll
                 for (int j = 0; j < K; ++j) u[b][j] |= (jh == j ? hm : 0u) | (W < 16 && jh + 1 == j ? hm2 : 0u);
             }
         }
+    };
+
+    // process side: the ICRC of the set whose last chunk is buffer b, from the final products
+    // fm (final_mul of its accumulator): result, trailer store, routing to the packet's lane
+    auto p_finish = [&](auto bc, uint32_t fm) __attribute__((always_inline)) {
+        constexpr int b = decltype(bc)::value;
+        const uint32_t crc = ~group_xor<W>(fm);
+        uint32_t r;
+        if constexpr (MODE == kCompute) r = crc;
+        else r = bperm(grp << Gm::LW, u[b][K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+        if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(p.base + cboff[b], 0, static_cast<int>(kQuadOOR), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs, static_cast<int>(ctr[b]), 0, 0);
+        }
+        if (cblk[b] != rb_block) {
+            if (rb_block >= 0 && got) store_result<MODE>(p, lo + static_cast<uint32_t>(rb_block) * 64u + lane, rbv);
+            got = false;
+            rb_block = cblk[b];
+        }
+        const uint32_t rt = ce[b] & 0xFFu;
+        const uint32_t v = bperm(rt & 63u, r);
+        if (rt != 0xFFu) {
+            rbv = v;
+            got = true;
+        }
+    };
+
+    // process side of one ring position: buffer b
+    auto p_consume = [&](auto bc) __attribute__((always_inline)) {
+        constexpr int b = decltype(bc)::value;
+        const int fl = cflags[b];
+        if (!(fl & (1 << 31))) return;
+        if constexpr (ABLATE != 5) p_masks(bc);  // diagnostic 5: no header masks
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            if constexpr (ABLATE == 1 || ABLATE == 3) acc ^= u[b][j];  // diagnostic: loads only / overhead only
+            if constexpr (ABLATE == 1 || ABLATE >= 3) acc ^= u[b][j];  // diagnostic: loads only / overhead only
             else acc = step_m64(lds, acc, u[b][j], c);
         }
         inflight -= 1;
         if (fl & (1 << 30)) {
-            const uint32_t crc = ~group_xor<W>(final_mul(lds, acc, c.fin));
-            acc = 0;
-            uint32_t r;
-            if constexpr (MODE == kCompute) r = crc;
-            else r = bperm(grp << Gm::LW, u[b][K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
-            if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
-                const __amdgpu_buffer_rsrc_t rs =
-                    __builtin_amdgcn_make_buffer_rsrc(p.base + cboff[b], 0, static_cast<int>(kQuadOOR), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs, static_cast<int>(ctr[b]), 0, 0);
-            }
-            if (cblk[b] != rb_block) {
-                if (rb_block >= 0 && got) store_result<MODE>(p, lo + static_cast<uint32_t>(rb_block) * 64u + lane, rbv);
-                got = false;
-                rb_block = cblk[b];
-            }
-            const uint32_t rt = ce[b] & 0xFFu;
-            const uint32_t v = bperm(rt & 63u, r);
-            if (rt != 0xFFu) {
-                rbv = v;
+            if constexpr (ABLATE == 4) {  // diagnostic 4: no final products / routing
+                rbv ^= acc;
                 got = true;
+                rb_block = cblk[b];
+            } else if constexpr (ABLATE == 6) {
+                p_finish(bc, acc);  // diagnostic 6: no final products
+            } else {
+                p_finish(bc, final_mul(lds, acc, c.fin));
             }
+            acc = 0;
         }
     };
 
@@ -500,6 +516,9 @@ __global__ __launch_bounds__(NT) void icrc_quad_kernel(BatchParams p) {
 // 21: K = 4, D = 6; 22 / 23: ablations of 20 (loads only / no loads, compute, ragged).
 // Oct (W = 8): 24: K = 10, D = 3; 25: K = 8, D = 4; 26: K = 5, D = 6; 27: K = 12, D = 3;
 // 28: K = 10, D = 4; 29: K = 17, D = 2; 30: K = 7, D = 5; 31 / 32: ablations of 24 (as 22 / 23).
+// 33 / 34: 24 at 8 waves per CU (occupancy probe; 34 without loads); 35: 24 without loads or
+// row steps (strided); 36 / 37 / 38: 35 without final products and routing / header masks / final
+// products.
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool ragged = p.off != nullptr || p.len != nullptr;
@@ -537,12 +556,16 @@ int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *str
         else ICRC_L512(8, kCompute, 10, 3, true, false, 2);
         return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
     }
-    if (variant == 22 || variant == 23 || variant == 31 || variant == 32 || variant == 35) {
+    if (variant == 22 || variant == 23 || variant == 31 || variant == 32 || variant == 35 || variant == 36 ||
+        variant == 37 || variant == 38) {
         if (variant == 22) ICRC_L(16, kCompute, 6, 4, true, false, 1);
         else if (variant == 23) ICRC_L(16, kCompute, 6, 4, true, false, 2);
         else if (variant == 31) ICRC_L(8, kCompute, 10, 3, true, false, 1);
         else if (variant == 32) ICRC_L(8, kCompute, 10, 3, true, false, 2);
-        else ICRC_L(8, kCompute, 10, 3, true, false, 3);
+        else if (variant == 35) ICRC_L(8, kCompute, 10, 3, false, false, 3);
+        else if (variant == 36) ICRC_L(8, kCompute, 10, 3, false, false, 4);
+        else if (variant == 38) ICRC_L(8, kCompute, 10, 3, false, false, 6);
+        else ICRC_L(8, kCompute, 10, 3, false, false, 5);
         return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
     }
     if (mode == kCompute) ICRC_QV(kCompute);

@@ -2,7 +2,7 @@
 """A/B the ICRC kernel variants in ONE process, interleaved rounds (methodology rule 24):
 C1 (1 Mi x 4156 B, strided) and C2 (mixed MTU, ragged) for each variant; checks that every
 variant returns identical ICRCs.  Prints one JSON line per (workload, variant)."""
-DIAGNOSTIC = {6, 7, 8, 9, 15, 18, 22, 23, 31, 32, 34, 35}  # ablations (loads-only / CRC-only): wrong results by design
+DIAGNOSTIC = {6, 7, 8, 9, 15, 18, 22, 23, 31, 32, 34, 35, 36, 37, 38}  # ablations (loads-only / CRC-only): wrong results by design
 import json
 import os
 import sys
