@@ -44,6 +44,9 @@ struct icrc_engine {
     uint32_t *d_table_quad = nullptr;
     uint32_t *d_table_oct = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // the long-packet half of a split batch runs here, beside the caller's
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    std::mutex fork_mu;  // orders the fork / join event pair between threads
     std::mutex mu;  // guards the host-batch stages
     Stage st[2];
 };
@@ -73,10 +76,12 @@ struct DeviceGuard {
 int grid_for(const icrc_engine *e, uint32_t n);
 
 // Launch a batch.  A variant forced on the engine runs alone.  Otherwise: a uniform strided
-// batch runs on the one-packet pipeline (variant 13) when its packets are long, on the quad
-// kernel when short; a ragged batch is split by length (hybrid dispatch): the quad kernel takes
-// L < kSplitLen (and every packet off the fast paths), the long-packet kernel the rest.
-int dispatch(const icrc_engine *e, int mode, BatchParams p, void *stream) {
+// batch runs on the one-packet pipeline (kDefaultVariant) when its packets are long, on the oct
+// kernel (kDefaultRaggedVariant) when short; a ragged batch is split by length (hybrid
+// dispatch): the oct kernel takes L < kSplitLen (and every packet off the fast paths) on the
+// caller's stream, the long-packet kernel the rest on the engine's side stream, forked from and
+// joined back into the caller's stream, so that each fills the other's tail.
+int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     const int grid = grid_for(e, p.n);
     p.split_len = 0;
     if (e->variant >= 0 && e->variant < icrc::kHybridVariantBase) {
@@ -90,8 +95,14 @@ int dispatch(const icrc_engine *e, int mode, BatchParams p, void *stream) {
     }
     p.variant = short_variant;
     p.split_len = icrc::kSplitLen;
-    const int rc = icrc::launch_batch(mode, p, grid, stream);
-    return rc != ICRC_OK ? rc : icrc::launch_long(mode, p, grid, stream);
+    std::lock_guard<std::mutex> g(e->fork_mu);
+    HIP_TRY(hipEventRecord(e->fork_ev, static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamWaitEvent(e->side, e->fork_ev, 0));
+    int rc = icrc::launch_batch(mode, p, grid, stream);
+    if (rc == ICRC_OK) rc = icrc::launch_long(mode, p, grid, e->side);
+    HIP_TRY(hipEventRecord(e->join_ev, e->side));
+    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), e->join_ev, 0));
+    return rc;
 }
 
 int grid_for(const icrc_engine *e, uint32_t n) {
@@ -377,7 +388,10 @@ int icrc_engine_create(int device, icrc_engine **out) {
         hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_table_oct, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table_oct, img_oct.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess) {
         icrc_engine_destroy(e);
         return ICRC_EDEVICE;
     }
@@ -390,11 +404,15 @@ int icrc_engine_destroy(icrc_engine *e) {
     {
         DeviceGuard g(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
+        if (e->side) (void)hipStreamSynchronize(e->side);
         for (Stage &s : e->st) stage_free(s);
         if (e->d_table) (void)hipFree(e->d_table);
         if (e->d_table_quad) (void)hipFree(e->d_table_quad);
         if (e->d_table_oct) (void)hipFree(e->d_table_oct);
         if (e->stream) (void)hipStreamDestroy(e->stream);
+        if (e->side) (void)hipStreamDestroy(e->side);
+        if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+        if (e->join_ev) (void)hipEventDestroy(e->join_ev);
     }
     {
         std::lock_guard<std::mutex> lk(g_registry_mu);
