@@ -763,3 +763,46 @@ def test_tiny_batches_every_path(engine, n):
     out, nerr, _ = run_batch(engine, buf, off, lens)
     assert nerr == 0
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
+
+
+def test_split_batches_concurrent_streams(engine):
+    """Split (hybrid) ragged batches issued from four host threads on four streams of one
+    engine: the fork / join onto the engine's side stream must keep every caller's long-packet
+    half ordered inside that caller's stream."""
+    import threading
+
+    rng = np.random.default_rng(4242)
+    jobs = []
+    for t in range(4):
+        n = 1500 + 100 * t
+        lens = rng.choice([316, 1084, 4156, 9000], n, p=[0.6, 0.2, 0.15, 0.05]).astype(np.uint32)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        buf = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
+        jobs.append((buf, off, lens, oracle_icrcs(buf, off, lens)))
+    errors = []
+
+    def worker(t):
+        try:
+            buf, off, lens, want = jobs[t]
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                d_buf, d_off, d_len = dev(buf), dev(off), dev(lens)
+                for _ in range(5):
+                    d_out = torch.zeros(len(lens), dtype=torch.int32, device="cuda")
+                    engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens),
+                                         d_out.data_ptr(), stream=s.cuda_stream)
+                    got = d_out.cpu().numpy().view(np.uint32)  # syncs this stream only
+                    if not np.array_equal(got, want):
+                        errors.append(f"thread {t}: {int((got != want).sum())} mismatches")
+                        return
+        except Exception as exc:  # noqa: BLE001
+            errors.append(f"thread {t}: {exc!r}")
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errors, errors
