@@ -88,7 +88,10 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
         p.variant = e->variant;
         return icrc::launch_batch(mode, p, grid, stream);
     }
-    const int short_variant = e->variant < 0 ? icrc::kDefaultRaggedVariant : e->variant - icrc::kHybridVariantBase;
+    const bool hybrid_forced = e->variant >= icrc::kHybridVariantBase && e->variant < icrc::kRxVariantBase;
+    p.long_variant = e->variant >= icrc::kHybridCompactBase && hybrid_forced ? 1 : 0;
+    const int short_variant = !hybrid_forced ? icrc::kDefaultRaggedVariant
+                            : e->variant - (p.long_variant ? icrc::kHybridCompactBase : icrc::kHybridVariantBase);
     if (p.off == nullptr && p.len == nullptr) {
         p.variant = p.ulen >= icrc::kSplitLen ? icrc::kDefaultVariant : short_variant;
         return icrc::launch_batch(mode, p, grid, stream);
@@ -449,9 +452,12 @@ int icrc_engine_default(int device, icrc_engine **out) {
 int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : ICRC_EINVAL; }
 
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
-    const bool hybrid = variant >= icrc::kHybridVariantBase + icrc::kFirstQuadVariant &&
-                        variant <= icrc::kHybridVariantBase + icrc::kMaxVariant;
-    if (!e || variant < -1 || (variant > icrc::kMaxVariant && !hybrid)) return ICRC_EINVAL;
+    const bool hybrid = (variant >= icrc::kHybridVariantBase + icrc::kFirstQuadVariant &&
+                         variant <= icrc::kHybridVariantBase + icrc::kMaxVariant) ||
+                        (variant >= icrc::kHybridCompactBase + icrc::kFirstQuadVariant &&
+                         variant <= icrc::kHybridCompactBase + icrc::kMaxVariant);
+    const bool rx = variant >= icrc::kRxVariantBase && variant <= icrc::kRxVariantBase + icrc::kMaxRxVariant;
+    if (!e || variant < -1 || (variant > icrc::kMaxVariant && !hybrid && !rx)) return ICRC_EINVAL;
     e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;
 }
@@ -572,6 +578,7 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     p.table = e->d_table;
     p.trailer = zero_trailer ? 1 : 0;
     p.rx = d_desc;
+    p.variant = e->variant >= icrc::kRxVariantBase ? e->variant - icrc::kRxVariantBase : 0;
     return icrc::launch_rx(p, grid_for(e, n), stream);
 }
 

@@ -48,6 +48,7 @@ struct BatchParams {
     const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 24-35)
     uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
                          // long-packet kernel (launch_long) L >= split_len
+    int long_variant;    // launch_long: 0 = filtered S = 2 pipeline (default), 1 = compacting S = 1 walker
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
@@ -58,6 +59,10 @@ constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
 constexpr uint32_t kSplitLen = 2048;
 // 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
 constexpr int kHybridVariantBase = 100;
+// 200 + q: the same with the compacting long-packet walker (A/B); 300 + r: receive-parse variant r.
+constexpr int kHybridCompactBase = 200;
+constexpr int kRxVariantBase = 300;
+constexpr int kMaxRxVariant = 2;
 constexpr int kMaxVariant = 38;  // 22, 23, 31-38: quad / oct ablations and probes (wrong results by design)
 
 enum Mode : int { kCompute = 0, kVerify = 1 };

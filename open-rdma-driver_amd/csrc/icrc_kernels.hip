@@ -74,6 +74,9 @@ __device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, 
     mb.block = block;
 }
 
+// LONG: the long-packet half of a split batch — packets with L < p.split_len belong to the short-
+// packet kernel and leave the slot empty (kind 0: no loads, no result).
+template <bool LONG = false>
 __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t lo,
                                           uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
     m.kind = 0;
@@ -94,6 +97,7 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
         off = static_cast<uint64_t>(lo + q) * p.stride;
         L = p.ulen;
     }
+    if (LONG && L < p.split_len) return;
     m.pkt = p.base + off;
     m.L = L;
     m.kind = 2;
@@ -332,7 +336,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
 // processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
 // ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
-template <int MODE, int S, int D, int ABL, bool PARSE = false>
+template <int MODE, int S, int D, int ABL, bool PARSE = false, bool LONG = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -353,7 +357,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
         if (static_cast<uint32_t>(d) < nsets) {
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
+                slot_meta<LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
                 slot_load<ABL>(m[d][s], lane, u[d][s]);
             }
         }
@@ -368,7 +372,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor)
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                slot_meta<LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
                 slot_load<ABL>(m[bp][s], lane, u[bp][s]);
             }
             const uint32_t q0 = ts * S;
@@ -475,7 +479,12 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
 }
 
-template <int MODE>
+// Default (COMPACT = false): per wave, the C1 pipeline (S = 2 chains, D = 1) over the wave's whole
+// chunk with short packets left as empty slots when long packets are dense — on an all-long ragged
+// batch it runs at the strided rate (1 Mi x 4156 B: 0.75 ms split vs 0.80-0.87 with the walker) —
+// and the compacting S = 1 walker above when they are sparse (on a mixed-MTU batch the dense walk
+// costs 1.32 ms against 0.49).  COMPACT = true: the walker always (A/B: variant 200 + q).
+template <int MODE, bool COMPACT>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -496,7 +505,20 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
+    if constexpr (COMPACT) {
+        run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
+    } else {
+        // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
+        // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
+        // (a mixed-MTU batch: ~1.5 % long) -> the compacting walker, which visits long packets only.
+        const uint32_t L0 = lane < nq ? (p.len ? p.len[lo + lane] : p.ulen) : 0u;
+        const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
+        const uint32_t nb = nq < 64u ? nq : 64u;
+        if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
+            run_pipelined<MODE, 2, 1, kStreamAux << 2, false, true>(p, lds, c, lane, lo, nq);
+        else
+            run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
+    }
 }
 
 // ---- row-stream path ------------------------------------------------------------------------
@@ -756,6 +778,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 
 // Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
 // words gathered from each packet's first two rows.
+template <int S, int D>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -777,7 +800,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, 2, 1, kStreamAux << 2, true>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, S, D, kStreamAux << 2, true>(p, lds, c, lane, lo, nq);
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
@@ -1288,8 +1311,14 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
 int launch_long(int mode, const BatchParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (mode == kCompute) hipLaunchKernelGGL(icrc_long_kernel<kCompute>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-    else hipLaunchKernelGGL(icrc_long_kernel<kVerify>, dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    const bool compact = p.long_variant == 1;
+    if (mode == kCompute) {
+        if (compact) hipLaunchKernelGGL((icrc_long_kernel<kCompute, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+        else hipLaunchKernelGGL((icrc_long_kernel<kCompute, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    } else {
+        if (compact) hipLaunchKernelGGL((icrc_long_kernel<kVerify, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+        else hipLaunchKernelGGL((icrc_long_kernel<kVerify, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    }
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
@@ -1313,7 +1342,12 @@ int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr,
 int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(icrc_rx_kernel, dim3(grid), dim3(kThreadsPerGroup), 0, static_cast<hipStream_t>(stream), p);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (p.variant) {  // A/B: 0 default (S = 2, D = 1), 1 (S = 1, D = 1), 2 (S = 1, D = 2)
+    case 1: hipLaunchKernelGGL((icrc_rx_kernel<1, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((icrc_rx_kernel<1, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    default: hipLaunchKernelGGL((icrc_rx_kernel<2, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    }
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -487,6 +487,29 @@ __device__ __forceinline__ void run_quad(const BatchParams &p, const char *lds, 
 template <int W, int MODE, int K, int D, bool RAGGED, bool TRAILER, int ABLATE = 0, int NT = kThreadsPerGroup>
 __global__ __launch_bounds__(NT) void icrc_quad_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
+    const uint32_t tw = gridDim.x * (NT / 64);
+    // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
+    uint32_t chunk = (p.n + tw - 1) / tw;
+    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + (64u / W - 1u)) & ~(64u / W - 1u);
+    if (RAGGED && p.split_len != 0 && p.len != nullptr) {
+        // Split batch: a workgroup whose packets are all the long-packet kernel's exits before
+        // its 160 KiB table load (an all-long ragged batch costs this kernel a length scan only).
+        const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * (NT / 64) * chunk;
+        const uint64_t g1 = g0 + static_cast<uint64_t>(NT / 64) * chunk;
+        const uint64_t end = g1 < p.n ? g1 : p.n;
+        bool any_short = false;
+        for (uint64_t i = g0 + threadIdx.x; i < end; i += NT) any_short |= p.len[i] < p.split_len;
+        // OR across the workgroup through the (not yet loaded) table space: the tables fill the
+        // whole LDS, so __syncthreads_or's own LDS word does not fit
+        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(lds4);
+        if (threadIdx.x == 0) *flag = 0u;
+        __syncthreads();
+        if (any_short) *flag = 1u;
+        __syncthreads();
+        const bool go = *flag != 0u;
+        __syncthreads();  // every wave has read the flag before the table load overwrites it
+        if (!go) return;
+    }
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(W == 16 ? p.table_quad : p.table_oct);
         for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += NT) lds4[i] = src[i];
@@ -498,11 +521,7 @@ __global__ __launch_bounds__(NT) void icrc_quad_kernel(BatchParams p) {
     LaneConsts c;
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
-    const uint32_t tw = gridDim.x * (NT / 64);
     const uint32_t gw = blockIdx.x * (NT / 64) + wave;
-    // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
-    uint32_t chunk = (p.n + tw - 1) / tw;
-    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + (64u / W - 1u)) & ~(64u / W - 1u);
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);

@@ -50,6 +50,44 @@ def main():
     for name, fn in cases.items():
         ms = timed(fn)
         print(json.dumps({"case": name, "ms": round(ms, 4), "GB/s": round(n * L / (ms * 1e-3) / 1e9, 1)}), flush=True)
+    # A/B (interleaved rounds): hybrid split with the filtered S = 2 long kernel (-1) vs the
+    # compacting walker (224), and the receive kernel's S / D variants (300-302)
+    wm = workloads.mixed_mtu_stream(4 << 20)
+    bm = workloads.synthesize(eng, wm, stream=s)
+    moff = torch.from_numpy(np.ascontiguousarray(wm.off)).cuda()
+    mln = torch.from_numpy(np.ascontiguousarray(wm.lens)).cuda()
+    mout = torch.zeros(wm.n, dtype=torch.int32, device="cuda")
+    mtot = int(wm.lens.astype(np.int64).sum())
+    c2 = lambda: eng.compute_batch(bm.data_ptr(), moff.data_ptr(), mln.data_ptr(), wm.n, mout.data_ptr(), False, 0, s)
+    ref_c2 = None
+    for rnd in range(3):
+        for v in (-1, 224):
+            eng.set_variant(v)
+            for name, fn, nb in (("verify_ragged", cases["verify_ragged"], n * L), ("compute_ragged", cases["compute_ragged"], n * L),
+                                 ("c2_hybrid", c2, mtot)):
+                ms = timed(fn)
+                print(json.dumps({"case": f"{name}_hyb{v}", "round": rnd, "ms": round(ms, 4),
+                                  "GB/s": round(nb / (ms * 1e-3) / 1e9, 1)}), flush=True)
+            torch.cuda.synchronize()
+            r = mout.cpu().numpy().copy()
+            if ref_c2 is None:
+                ref_c2 = r
+            print(json.dumps({"case": f"c2_same_{v}", "ok": bool((r == ref_c2).all())}), flush=True)
+        for v in (300, 301, 302):
+            eng.set_variant(v)
+            for name in ("rx_ragged", "rx_strided"):
+                ms = timed(cases[name])
+                print(json.dumps({"case": f"{name}_v{v}", "round": rnd, "ms": round(ms, 4),
+                                  "GB/s": round(n * L / (ms * 1e-3) / 1e9, 1)}), flush=True)
+    eng.set_variant(-1)
+    # forced single-kernel variants on the ragged batch (no hybrid split): where the ragged loss is
+    for v in (16, 13, 14):
+        eng.set_variant(v)
+        for name in ("verify_ragged", "compute_ragged"):
+            ms = timed(cases[name])
+            print(json.dumps({"case": f"{name}_v{v}", "ms": round(ms, 4),
+                              "GB/s": round(n * L / (ms * 1e-3) / 1e9, 1)}), flush=True)
+    eng.set_variant(-1)
 
 
 if __name__ == "__main__":

@@ -144,11 +144,12 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [-1, 19, 20, 21, 24, 25, 26, 120])
+@pytest.mark.parametrize("variant", [-1, 19, 20, 21, 24, 25, 26, 120, 224])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
 def test_quad_block_transitions_compute_verify(engine, variant, n):
     """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
-    one-packet pipeline for the rest; 120: the same with quad) on contrasting 64-packet blocks: compute with trailer
+    one-packet pipeline for the rest; 120: the same with quad; 224: oct with the compacting long-packet
+    walker) on contrasting 64-packet blocks: compute with trailer
     write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
     trailer zeroing."""
     rng = np.random.default_rng((variant % 100 + 2) * 1000 + n)
@@ -183,6 +184,55 @@ def test_quad_block_transitions_compute_verify(engine, variant, n):
             assert not after[t: t + 4].any()
     finally:
         engine.set_variant(-1)
+
+
+def test_split_batch_dense_and_sparse_waves(engine):
+    """Hybrid dispatch at a size where every wave owns whole 64-packet blocks: waves whose first
+    block is mostly long take the dense long-packet pipeline (short packets as empty slots), the
+    others the compacting walker; workgroups with no short packet skip the oct kernel.  Blocks of
+    64: all long / long with a few short and irregular packets / mostly short / all short, in runs
+    so that whole workgroups are all long.  Compute with trailer write, then verify with negatives."""
+    rng = np.random.default_rng(4242)
+    nblk = 5000  # 320 000 packets: > 64 per wave on a 256-CU grid
+    kinds = np.repeat(rng.integers(0, 4, nblk // 40), 40)[:nblk]
+    kinds[:1200] = 0  # the first workgroups: long packets only
+    lens, gaps = [], []
+    for k in kinds:
+        if k == 0:
+            ln, gp = rng.choice([2048, 2052, 3000, 4156], 64), np.zeros(64, int)
+        elif k == 1:
+            ln, gp = np.full(64, 4156), np.zeros(64, int)
+            ln[rng.integers(0, 64, 6)] = rng.choice([44, 316, 1084], 6)
+            gp[rng.integers(0, 64, 2)] = 1  # irregular offsets
+            ln[rng.integers(0, 64, 1)] = 4157  # L % 4 != 0
+        elif k == 2:
+            ln, gp = rng.choice([60, 316, 1084], 64), np.zeros(64, int)
+            ln[rng.integers(0, 64, 2)] = 4156
+        else:
+            ln, gp = rng.integers(11, 511, 64) * 4, np.zeros(64, int)
+        lens.append(ln)
+        gaps.append(gp)
+    lens = np.concatenate(lens).astype(np.uint32)
+    gaps = np.concatenate(gaps).astype(np.uint64)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    n = lens.size
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    out, nerr, wrote = run_batch(engine, buf, off, lens, write_trailer=True)
+    assert nerr == 0
+    want = oracle_icrcs(buf, off, lens)
+    np.testing.assert_array_equal(out, want)
+    bad = np.arange(0, n, 101)
+    for i in bad:
+        wrote[int(off[i]) + 36 + int(rng.integers(0, int(lens[i]) - 40))] ^= 0x04
+    d_buf, d_off, d_len = dev(wrote), dev(off), dev(lens)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(),
+                        stream=stream_handle())
+    torch.cuda.synchronize()
+    expect = np.ones(n, np.uint8)
+    expect[bad] = 0
+    np.testing.assert_array_equal(d_ok.cpu().numpy(), expect)
 
 
 def test_max_and_boundary_lengths(engine):
@@ -551,13 +601,23 @@ def assert_desc_equal(got, want):
         np.testing.assert_array_equal(got[f], want[f], err_msg=f)
 
 
+@pytest.mark.parametrize("rx_variant", [-1, 301, 302])
 @pytest.mark.parametrize("layout", ["packed", "aligned"])
 @pytest.mark.parametrize("zero_trailer", [False, True])
-def test_rx_parse_matches_oracle(engine, layout, zero_trailer):
+def test_rx_parse_matches_oracle(engine, layout, zero_trailer, rx_variant):
     """Every opcode x pad, corrupted opcode / transport / length / ICRC; packed offsets put most
-    packets on the byte-wise path, aligned ones on the row stream."""
+    packets on the byte-wise path, aligned ones on the row stream.  rx_variant: the default receive
+    kernel (S = 2 chains) and the A/B builds 301 (S = 1) and 302 (S = 1, two sets in flight)."""
     import rx_cases
 
+    engine.set_variant(rx_variant)
+    try:
+        _rx_parse_case(engine, layout, zero_trailer, rx_cases)
+    finally:
+        engine.set_variant(-1)
+
+
+def _rx_parse_case(engine, layout, zero_trailer, rx_cases):
     rng = np.random.default_rng(7)
     pkts = rx_cases.make_packets(rng)
     sizes = [p.size for p in pkts]
