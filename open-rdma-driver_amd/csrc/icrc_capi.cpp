@@ -578,8 +578,24 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     p.table = e->d_table;
     p.trailer = zero_trailer ? 1 : 0;
     p.rx = d_desc;
-    p.variant = e->variant >= icrc::kRxVariantBase ? e->variant - icrc::kRxVariantBase : 0;
-    return icrc::launch_rx(p, grid_for(e, n), stream);
+    const int rxv = e->variant >= icrc::kRxVariantBase ? e->variant - icrc::kRxVariantBase : 0;
+    if (rxv != 0) {  // A/B: the fused single-pass kernel
+        p.variant = rxv;
+        return icrc::launch_rx(p, grid_for(e, n), stream);
+    }
+    // Two passes (icrc_kernels.hip, icrc_rx_desc_kernel): the verify dispatch writes the ok bytes
+    // (into d_ok, or a stream-ordered scratch array when the caller passes none), then the
+    // descriptors are built from the header words and those bytes.
+    p.table_quad = e->d_table_quad;
+    p.table_oct = e->d_table_oct;
+    uint8_t *scratch = nullptr;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!d_ok) HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&scratch), n, s));
+    p.ok = d_ok ? d_ok : scratch;
+    int rc = dispatch(e, icrc::kVerify, p, stream);
+    if (rc == ICRC_OK) rc = icrc::launch_rx_desc(p, e->num_cu, stream);
+    if (scratch && hipFreeAsync(scratch, s) != hipSuccess && rc == ICRC_OK) rc = ICRC_EDEVICE;
+    return rc;
 }
 
 int icrc_ipv4_checksum_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off, uint64_t stride, uint32_t n,

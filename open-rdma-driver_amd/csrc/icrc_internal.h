@@ -59,10 +59,11 @@ constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
 constexpr uint32_t kSplitLen = 2048;
 // 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
 constexpr int kHybridVariantBase = 100;
-// 200 + q: the same with the compacting long-packet walker (A/B); 300 + r: receive-parse variant r.
+// 200 + q: the same with the compacting long-packet walker (A/B); 300 + r: receive-parse variant r
+// (0 two-pass default, 1 fused S = 2, 2 fused S = 1 D = 2, 3 fused diagnostic).
 constexpr int kHybridCompactBase = 200;
 constexpr int kRxVariantBase = 300;
-constexpr int kMaxRxVariant = 2;
+constexpr int kMaxRxVariant = 3;  // 3: diagnostic (raw header words, wrong descriptors by design)
 constexpr int kMaxVariant = 38;  // 22, 23, 31-38: quad / oct ablations and probes (wrong results by design)
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
@@ -74,7 +75,10 @@ constexpr int kThreadsPerGroup = 64 * kWavesPerGroup;
 int launch_batch(int mode, const BatchParams &p, int grid, void *stream);
 // One-packet pipeline over the packets with L >= p.split_len of a ragged batch (hybrid dispatch).
 int launch_long(int mode, const BatchParams &p, int grid, void *stream);
-int launch_rx(const BatchParams &p, int grid, void *stream);  // verify + parse (p.rx)
+int launch_rx(const BatchParams &p, int grid, void *stream);  // fused verify + parse (p.rx), variants 1-3
+// Receive parse pass 2 (the default path): descriptors from the header words, icrc_ok read from
+// p.ok where the verify pass left it.
+int launch_rx_desc(const BatchParams &p, int num_cu, void *stream);
 // Quad kernel (icrc_quad.hip), variant 19..21 (chunk size / chunks in flight).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,

@@ -246,7 +246,8 @@ __device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row
 
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
 // the wave's result buffer.
-template <int MODE, int S, int ABL, bool PARSE = false>
+// PARSE: 0 off; 1 receive parse (rx_store); 3 diagnostic: the raw header words stored, no decode.
+template <int MODE, int S, int ABL, int PARSE = 0>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
                                             uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows],
                                             uint32_t q0, ResultBuf &rb, uint32_t lo = 0) {
@@ -316,8 +317,11 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             if (m[s].kind == 1) {
                 const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
                 rb_put(rb, q0 + s, r);
-                if constexpr (PARSE)
+                if constexpr (PARSE == 3) {
+                    if (lane < 18u) reinterpret_cast<uint32_t *>(p.rx + lo + q0 + s)[lane] = hdr[s] ^ r;
+                } else if constexpr (PARSE) {
                     rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
+                }
             }
     }
 #pragma unroll
@@ -336,7 +340,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
 // processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
 // ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
-template <int MODE, int S, int D, int ABL, bool PARSE = false, bool LONG = false>
+template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -515,7 +519,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, kStreamAux << 2, false, true>(p, lds, c, lane, lo, nq);
+            run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true>(p, lds, c, lane, lo, nq);
         else
             run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
     }
@@ -778,7 +782,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 
 // Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
 // words gathered from each packet's first two rows.
-template <int S, int D>
+template <int S, int D, int PARSE = 1>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -800,7 +804,124 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, S, D, kStreamAux << 2, true>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, S, D, kStreamAux << 2, PARSE>(p, lds, c, lane, lo, nq);
+}
+
+// ---- receive parse, pass 2 (icrc_rx_parse_device default) ----------------------------------
+// Why two passes: on gfx950 VMEM loads and stores share vmcnt, and with both kinds in flight the
+// compiler can only wait for zero — a 72-byte descriptor store per packet inside the CRC pipeline
+// drains its prefetch every packet (the fused kernel: 0.84-0.92 ms on 1 Mi x 4156 B against 0.70
+// for verify alone; storing the raw header words without any decode costs the same).  So pass 1 is
+// the plain verify dispatch into the caller's ok array (or a stream-ordered scratch array), and
+// this pass re-reads each packet's first 72 bytes (~2 % of the packet bytes) and
+// writes the descriptors.  A wave takes 64 packets: header words are loaded three packets per
+// instruction (18 lanes each, contiguous), transposed through LDS to lane = packet for the decode
+// (to_rdma_message, packet_processor.rs:18-71, as rx_store), and transposed back so the 64
+// descriptors (4608 contiguous bytes) leave as 18 coalesced dword stores.
+constexpr uint32_t kRxStride = 19;  // LDS words per packet row (odd: conflict-free lane = packet reads)
+
+__global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
+    __shared__ uint32_t sh_all[4 * 64 * kRxStride];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *sh = sh_all + wave * 64u * kRxStride;
+    const uint32_t tw = gridDim.x * 4u;
+    const uint32_t g = lane / 18u, w = lane - 18u * g;  // header-load layout: packet group, word
+    for (uint32_t base = (blockIdx.x * 4u + wave) * 64u; base < p.n; base += tw * 64u) {
+        const uint32_t i = base + lane;
+        const bool in = i < p.n;
+        const uint64_t off = in ? (p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride) : 0u;
+        const uint32_t L = in ? (p.len ? p.len[i] : p.ulen) : 0u;
+        const uint32_t okb = in ? p.ok[i] : 0u;  // from the verify pass
+        const uint8_t *pkt = p.base + off;
+        const bool fast = L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
+        const uint32_t olo = static_cast<uint32_t>(off), ohi = static_cast<uint32_t>(off >> 32);
+        const uint32_t lf = fast ? L : 0u;  // 0: not loaded here (short / irregular)
+#pragma unroll
+        for (uint32_t r = 0; r < 22; ++r) {  // 3 packets per round, 66 >= 64
+            const uint32_t j = 3u * r + g;
+            const int src = static_cast<int>((j & 63u) << 2);
+            const uint32_t jl = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lf)));
+            const uint32_t jlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(olo)));
+            const uint32_t jhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ohi)));
+            uint32_t v = 0u;
+            if (g < 3u && j < 64u && 4u * w + 8u <= jl) {  // jl = 0 for packets not on this path
+                const uint8_t *q = p.base + (static_cast<uint64_t>(jlo) | (static_cast<uint64_t>(jhi) << 32));
+                v = reinterpret_cast<const uint32_t *>(q)[w];
+            }
+            if (g < 3u && j < 64u) sh[j * kRxStride + w] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t h[18];
+#pragma unroll
+        for (uint32_t k = 0; k < 18; ++k) h[k] = sh[lane * kRxStride + k];
+        if (!fast && L >= ICRC_MIN_PACKET) {  // misaligned or L % 4 != 0: byte-wise, this lane only
+#pragma unroll
+            for (uint32_t k = 0; k < 18; ++k) {
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const uint32_t o = 4u * k + t;
+                    x |= (o + 4u < L ? static_cast<uint32_t>(pkt[o]) : 0u) << (8u * t);
+                }
+                h[k] = x;
+            }
+        }
+        const bool valid = L >= ICRC_MIN_PACKET;
+        const uint32_t w7 = h[7], w9 = h[9], w10 = h[10];
+        const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+        // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
+        const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                          : (op == 0x0Cu)                 ? 44u
+                          : (op == 0x11u)                 ? 16u
+                          : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                          : 0u;
+        const uint32_t status = !valid                  ? ICRC_RX_TRUNCATED
+                              : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
+                              : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
+                              : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
+                                                        : ICRC_RX_OK;
+        const bool ack = hs == 16u;
+        const bool ok = status == ICRC_RX_OK;
+        const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                               (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                               (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+        const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+        const uint64_t poff = off + 28u + hs;
+        // present classes: General metadata has a RETH, Acknowledge an AETH; none on error
+        const bool reth = ok && !ack, sec = ok && hs == 44u, imm = ok && hs == 32u, aeth = ok && ack;
+        uint32_t v[18];
+        v[0] = reth ? bswap32(h[11]) : 0u;  // RETH va (big-endian u64, bytes 40-47)
+        v[1] = reth ? bswap32(h[10]) : 0u;
+        v[2] = sec ? bswap32(h[15]) : 0u;   // secondary RETH va (bytes 56-63)
+        v[3] = sec ? bswap32(h[14]) : 0u;
+        v[4] = ok ? static_cast<uint32_t>(poff) : 0u;
+        v[5] = ok ? static_cast<uint32_t>(poff >> 32) : 0u;
+        v[6] = ok ? L - 32u - hs - pad : 0u;
+        v[7] = reth ? bswap32(h[12]) : 0u;  // rkey, dlen
+        v[8] = reth ? bswap32(h[13]) : 0u;
+        v[9] = sec ? bswap32(h[16]) : 0u;
+        v[10] = sec ? bswap32(h[17]) : 0u;
+        v[11] = imm ? bswap32(h[14]) : 0u;
+        v[12] = ok ? bswap32(h[8]) & 0xFFFFFFu : 0u;     // dqpn
+        v[13] = ok ? bswap32(h[9]) & 0xFFFFFFu : 0u;     // psn
+        v[14] = aeth ? bswap32(h[10]) & 0xFFFFFFu : 0u;  // AETH msn
+        v[15] = ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u;
+        v[16] = ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u;
+        v[17] = (okb & 0xFFu) | (status << 8);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t k = 0; k < 18; ++k) sh[lane * kRxStride + k] = v[k];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t cnt = p.n - base < 64u ? p.n - base : 64u;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(p.rx + base);
+#pragma unroll
+        for (uint32_t t = 0; t < 18; ++t) {
+            const uint32_t idx = t * 64u + lane, pk = idx / 18u, k = idx - 18u * pk;
+            if (pk < cnt) dst[idx] = sh[pk * kRxStride + k];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
@@ -1343,11 +1464,20 @@ int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    switch (p.variant) {  // A/B: 0 default (S = 2, D = 1), 1 (S = 1, D = 1), 2 (S = 1, D = 2)
-    case 1: hipLaunchKernelGGL((icrc_rx_kernel<1, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    switch (p.variant) {  // A/B: 1 (S = 2, D = 1), 2 (S = 1, D = 2), 3 diagnostic (raw header words)
     case 2: hipLaunchKernelGGL((icrc_rx_kernel<1, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 3: hipLaunchKernelGGL((icrc_rx_kernel<2, 1, 3>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     default: hipLaunchKernelGGL((icrc_rx_kernel<2, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     }
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_rx_desc(const BatchParams &p, int num_cu, void *stream) {
+    if (p.n == 0) return ICRC_OK;
+    const uint64_t want = (static_cast<uint64_t>(p.n) + 255u) / 256u;
+    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u;  // 64 waves per CU
+    const int grid = static_cast<int>(want < cap ? want : cap);
+    hipLaunchKernelGGL(icrc_rx_desc_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

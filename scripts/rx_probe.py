@@ -60,7 +60,7 @@ def main():
     mtot = int(wm.lens.astype(np.int64).sum())
     c2 = lambda: eng.compute_batch(bm.data_ptr(), moff.data_ptr(), mln.data_ptr(), wm.n, mout.data_ptr(), False, 0, s)
     ref_c2 = None
-    for rnd in range(3):
+    for rnd in range(2):
         for v in (-1, 224):
             eng.set_variant(v)
             for name, fn, nb in (("verify_ragged", cases["verify_ragged"], n * L), ("compute_ragged", cases["compute_ragged"], n * L),

@@ -601,13 +601,14 @@ def assert_desc_equal(got, want):
         np.testing.assert_array_equal(got[f], want[f], err_msg=f)
 
 
-@pytest.mark.parametrize("rx_variant", [-1, 301, 302])
+@pytest.mark.parametrize("rx_variant", [-1, 301, 302])  # two-pass default, fused S = 2, fused S = 1
 @pytest.mark.parametrize("layout", ["packed", "aligned"])
 @pytest.mark.parametrize("zero_trailer", [False, True])
 def test_rx_parse_matches_oracle(engine, layout, zero_trailer, rx_variant):
     """Every opcode x pad, corrupted opcode / transport / length / ICRC; packed offsets put most
     packets on the byte-wise path, aligned ones on the row stream.  rx_variant: the default receive
-    kernel (S = 2 chains) and the A/B builds 301 (S = 1) and 302 (S = 1, two sets in flight)."""
+    path (verify dispatch, then descriptors from the header words) and the fused single-pass kernel
+    (301: S = 2 chains, 302: S = 1, two sets in flight)."""
     import rx_cases
 
     engine.set_variant(rx_variant)
@@ -635,11 +636,15 @@ def _rx_parse_case(engine, layout, zero_trailer, rx_cases):
     np.testing.assert_array_equal(after, ref)
 
 
-def test_rx_parse_c1_stream(engine):
-    """A 4 KiB WRITE_MIDDLE stream (strided, no offset array) with one flipped bit per 1024."""
+@pytest.mark.parametrize("ragged", [False, True])
+@pytest.mark.parametrize("rx_variant", [-1, 301])
+def test_rx_parse_c1_stream(engine, ragged, rx_variant):
+    """A 4 KiB WRITE_MIDDLE stream (strided, or the same packets through offset / length arrays) with
+    one flipped bit per 1024; the ok bytes go to d_ok as well.  70 000 packets: every wave of the
+    grid owns whole 64-packet blocks."""
     import icrc_amd
 
-    n = 4096
+    n = 70000
     buf, off, lens = oracle.synth_middle_stream(n, psn0=0xFFFF00)
     L = int(lens[0])
     for i in range(0, n, 1024):
@@ -647,11 +652,23 @@ def test_rx_parse_c1_stream(engine):
     want = oracle.rx_parse(buf.copy(), off, lens)
     d_buf = dev(buf)
     d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
-    engine.rx_parse(d_buf.data_ptr(), 0, 0, n, d_desc.data_ptr(), stride=L, length=L, stream=stream_handle())
-    torch.cuda.synchronize()
+    d_ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    engine.set_variant(rx_variant)
+    try:
+        if ragged:
+            d_off, d_len = dev(np.asarray(off, np.uint64)), dev(np.asarray(lens, np.uint32))
+            engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(),
+                            d_ok.data_ptr(), stream=stream_handle())
+        else:
+            engine.rx_parse(d_buf.data_ptr(), 0, 0, n, d_desc.data_ptr(), d_ok.data_ptr(), stride=L, length=L,
+                            stream=stream_handle())
+        torch.cuda.synchronize()
+    finally:
+        engine.set_variant(-1)
     got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
     assert_desc_equal(got, want)
-    assert int(np.sum(got["icrc_ok"] == 0)) == n // 1024
+    np.testing.assert_array_equal(d_ok.cpu().numpy(), got["icrc_ok"])
+    assert int(np.sum(got["icrc_ok"] == 0)) == (n + 1023) // 1024
     assert np.all(got["payload_len"] == 4096) and np.all(got["status"] == 0)
 
 
