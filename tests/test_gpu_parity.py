@@ -144,12 +144,12 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [-1, 19, 20, 21, 24, 25, 26, 120, 224])
+@pytest.mark.parametrize("variant", [-1, 19, 20, 21, 24, 25, 26, 120, 124, 224])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
 def test_quad_block_transitions_compute_verify(engine, variant, n):
     """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
-    one-packet pipeline for the rest; 120: the same with quad; 224: oct with the compacting long-packet
-    walker) on contrasting 64-packet blocks: compute with trailer
+    one-packet pipeline for the rest, or at these sizes the one-packet pipeline alone; 124 / 120: the
+    split forced, with oct / quad; 224: oct with the compacting long-packet walker) on contrasting 64-packet blocks: compute with trailer
     write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
     trailer zeroing."""
     rng = np.random.default_rng((variant % 100 + 2) * 1000 + n)
@@ -799,11 +799,12 @@ def test_empty_batches_are_noops(engine):
     assert icrc_amd.compute_icrc_batch(np.zeros(0, np.uint8), [], []).size == 0
 
 
-@pytest.mark.parametrize("variant", [-1, 120])
+@pytest.mark.parametrize("variant", [-1, 120, 124])
 @pytest.mark.parametrize("pmtu", [256, 1024])
 def test_short_strided_stream_quad_path(engine, pmtu, variant):
-    """Uniform strided batches of short packets go to the oct (-1) or quad (120) kernel
-    (non-ragged variant): compute, trailer write and verify against the oracle."""
+    """Uniform strided batches of short packets (at this size the one-packet pipeline by default;
+    forced to the quad (120) or oct (124) kernel, non-ragged variant): compute, trailer write and
+    verify against the oracle."""
     n = 2000 + pmtu // 256  # not a multiple of 4 or 64
     buf, off, lens = oracle.synth_middle_stream(n, pmtu=pmtu)
     L = int(lens[0])
@@ -829,15 +830,21 @@ def test_short_strided_stream_quad_path(engine, pmtu, variant):
     assert bool((d_ok == 1).all().item())
 
 
+@pytest.mark.parametrize("variant", [-1, 124])
 @pytest.mark.parametrize("n", [1, 2, 3, 5])
-def test_tiny_batches_every_path(engine, n):
-    """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block."""
+def test_tiny_batches_every_path(engine, n, variant):
+    """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block;
+    the default (one-packet pipeline at this size) and the split forced (124)."""
     rng = np.random.default_rng(900 + n)
     lens = rng.choice([44, 316, 1084, 4156, 9000], n).astype(np.uint32)
     off = np.zeros(n, np.uint64)
     off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
     buf = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
-    out, nerr, _ = run_batch(engine, buf, off, lens)
+    engine.set_variant(variant)
+    try:
+        out, nerr, _ = run_batch(engine, buf, off, lens)
+    finally:
+        engine.set_variant(-1)
     assert nerr == 0
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
@@ -851,7 +858,7 @@ def test_split_batches_concurrent_streams(engine):
     rng = np.random.default_rng(4242)
     jobs = []
     for t in range(4):
-        n = 1500 + 100 * t
+        n = 5000 + 500 * t  # above one packet per wave of the grid: the split (fork / join) path
         lens = rng.choice([316, 1084, 4156, 9000], n, p=[0.6, 0.2, 0.15, 0.05]).astype(np.uint32)
         off = np.zeros(n, np.uint64)
         off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
