@@ -228,11 +228,19 @@ def test_split_batch_dense_and_sparse_waves(engine):
     d_buf, d_off, d_len = dev(wrote), dev(off), dev(lens)
     d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
     engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(),
-                        stream=stream_handle())
+                        zero_trailer=True, stream=stream_handle())
     torch.cuda.synchronize()
     expect = np.ones(n, np.uint8)
     expect[bad] = 0
     np.testing.assert_array_equal(d_ok.cpu().numpy(), expect)
+    # zero_trailer (deferred trailer pass at this size): every trailer zeroed, nothing else touched
+    after = d_buf.cpu().numpy()
+    tpos = (off + lens.astype(np.uint64) - 4).astype(np.int64)
+    idx = tpos[:, None] + np.arange(4)[None, :]
+    assert not after[idx].any()
+    keep = np.ones(after.size, bool)
+    keep[idx.ravel()] = False
+    np.testing.assert_array_equal(after[keep], wrote[keep])
 
 
 def test_max_and_boundary_lengths(engine):
