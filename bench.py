@@ -6,21 +6,38 @@ IPv4 20 + UDP 8 + BTH 12 + RETH 16 + 4096 payload + ICRC 4), synthesised on the 
 the reference's PacketWriter field layout; one "step" = one ICRC-compute pass (kernel launch)
 over the whole batch, inputs resident in HBM, ICRCs written to an HBM array.
 
-Multi-GPU (--gpus N via torch.distributed.run): one process per GPU, each with its own
-independent QP stream of 1 Mi packets (configs[4], weak scaling, no collective on the
-data path; the only collectives are the timing barrier and a max over ranks).
+Multi-GPU (configs[4]): one process per GPU, no collective on the data path.
+  * `python bench.py --gpus N` with no WORLD_SIZE in the environment starts
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a CHILD process
+    (before anything touches a GPU) and exits with its status; under torch.distributed.run
+    WORLD_SIZE must equal --gpus, and every rank must have a GPU of its own, or bench exits
+    non-zero.
+  * --scaling weak (default): every rank runs its own independent QP stream of --packets
+    packets (dqpn = 2 + rank).  --scaling strong: --packets packets in total, split into
+    contiguous shards (shard.shard_range) of one stream.
+  * value = bytes of every rank / the slowest rank's time (shard.aggregate: one MAX and one
+    SUM all-reduce of scalars, outside the timed region).
+
+Every rank checks a sample of its ICRCs against the CPU restatement (oracle/, the checker;
+outside the timed region); the failures are summed over ranks and bench exits 1 if any.
 
 Prints ONE JSON line (rank 0).  value = whole-job GiB/s of packet bytes (sum of L, which
 equals the algorithmic bytes: L-4 read + 4 written per packet).  roofline = the ICRC kernel's
 achieved GB/s (HIP events on the launch stream) vs the 8.0 TB/s HBM3E peak.  cpu_baseline =
 the CPU port of compute_icrc with a crc32fast-equivalent PCLMULQDQ core (oracle/icrc_fast.c),
 rank 0 / N=1 only, on a bounded sample of the same packets.
+
+--cpu-stub (tests only): the same launcher, rank handling, barriers and aggregation on gloo
+with a CPU stand-in step (zlib.crc32 of every packet, not the ICRC and not the product), so
+the N>1 plumbing is exercised on a machine without GPUs (tests/test_multi_rank.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,29 +45,252 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "open-rdma-driver_amd"), os.path.join(ROOT, "oracle")]
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 GIB = float(1 << 30)
+METRIC = "device-resident ICRC GiB/s over 4 KiB-MTU packet batches; % of HBM-read roofline"
 
 
 def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--packets", type=int, default=1 << 20,
+                    help="packets per GPU (weak scaling) or in total (strong scaling)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--pmtu", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (the parity sample still runs)")
+    ap.add_argument("--check-packets", type=int, default=2048,
+                    help="per rank: packets at each end of the shard checked against the CPU restatement")
     ap.add_argument("--extra", action="store_true",
-                    help="also time verify, mixed-MTU, 16 MiB round trip and the host-resident path")
-    return ap.parse_args()
+                    help="also time verify, trailer stores, mixed-MTU, 16 MiB round trip, packetizer, receive "
+                         "parse and the host-resident path")
+    ap.add_argument("--cpu-stub", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--inject-fault-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+# ---- launcher ------------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 without torch.distributed.run around us: start it as a child process (no
+    exec, nothing has touched a GPU here) and return its exit status."""
+    if not args.cpu_stub:
+        import torch  # device_count() does not initialise the GPU on this image
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible; refusing to report a "
+                f"{have}-GPU number as {args.gpus}")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    log("bench.py: launching " + " ".join(cmd[1:]))
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ---- timing --------------------------------------------------------------------------------
+def time_steps(fn, steps: int, warmup: int, world: int, sync, barrier):
+    """Warmup, barrier + sync, K timed steps, sync + barrier.  Returns (this rank's wall seconds,
+    kernel ms per step from HIP events on the launch stream or None)."""
+    for _ in range(warmup):
+        fn()
+    sync()
+    if world > 1:
+        barrier()
+    sync()
+    ev = None
+    if not ARGS.cpu_stub:
+        import torch
+
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    t0 = time.perf_counter()
+    if ev:
+        ev[0].record()
+    for _ in range(steps):
+        fn()
+    if ev:
+        ev[1].record()
+    sync()
+    if world > 1:
+        barrier()
+    sync()
+    wall = time.perf_counter() - t0
+    return wall, (ev[0].elapsed_time(ev[1]) / steps if ev else None)
+
+
+def time_kernel(fn, steps: int, warmup: int, world: int):
+    """GPU launches: (wall seconds of this rank, kernel ms per launch)."""
+    import torch
+    import torch.distributed as dist
+
+    return time_steps(fn, steps, warmup, world, torch.cuda.synchronize, dist.barrier)
+
+
+ARGS = None
+
+
+def main(argv=None) -> int:
+    global ARGS
+    argv = sys.argv[1:] if argv is None else argv
+    args = ARGS = parse(argv)
+    if args.gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+        return 2
+    if args.cpu_stub:
+        return run_cpu_stub(args, rank, world)
+    return run_gpu(args, rank, world, local)
+
+
+# ---- the GPU run ---------------------------------------------------------------------------
+def run_gpu(args, rank: int, world: int, local: int) -> int:
+    import torch
+    import torch.distributed as dist
+
+    if local >= torch.cuda.device_count():
+        log(f"bench.py: rank {rank} (local {local}) has no GPU of its own "
+            f"({torch.cuda.device_count()} visible)")
+        return 2
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import icrc_amd
+    from icrc_amd import shard, workloads
+
+    eng = icrc_amd.Engine(local)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # ---- C1 workload: weak = one QP stream per rank; strong = a shard of one stream ----
+    if args.scaling == "weak":
+        sp = shard.stream_params(rank)
+        w = workloads.write_middle_stream(args.packets, args.pmtu, dqpn=sp.dqpn, payload_key=sp.payload_key)
+    else:
+        lo, hi = shard.shard_range(args.packets, rank, world)
+        w = workloads.subset(workloads.write_middle_stream(args.packets, args.pmtu), lo, hi)
+    n = w.n
+    L = int(w.lens[0])
+    d_buf = workloads.synthesize(eng, w, stream=stream)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), False, stream)
+
+    wall, kms = time_kernel(step, args.steps, args.warmup, world)
+    bytes_per_step = n * L
+
+    # ---- CPU leg (outside the timed region): the parity sample on every rank; the CPU
+    # baseline on rank 0 at N = 1.  The oracle is the checker / CPU port here only. ----
+    import oracle as orc
+
+    fails, checked = check_sample(orc, d_buf, d_out, n, L, args.check_packets, rank, args.inject_fault_rank)
+    agg = shard.aggregate(bytes_per_step * args.steps, wall, fails)
+    achieved = bytes_per_step / (kms * 1e-3) / 1e9
+
+    result = {
+        "metric": METRIC,
+        "value": round(agg.gib_per_s, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(agg.seconds / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-synthesised RDMA WRITE_MIDDLE packets, splitmix64 payload)",
+        "config": {
+            "workload": ("configs[1]: 1Mi x 4KiB-MTU packets per GPU, device-resident ICRC compute"
+                         if world == 1 else
+                         f"configs[4]: {world} independent QP streams, one per GPU, {args.packets} packets each"
+                         if args.scaling == "weak" else
+                         f"configs[4] strong scaling: {args.packets} packets of one stream split {world} ways"),
+            "packets_per_gpu": n,
+            "packets_total_per_step": agg.total_bytes // args.steps // L,
+            "packet_bytes": L,
+            "pmtu": args.pmtu,
+            "bytes_per_gpu_per_step": bytes_per_step,
+            "bytes_total_per_step": agg.total_bytes // args.steps,
+            "parallelism": f"shard-per-gpu x{world} (no collective on the data path)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "icrc_batch_kernel<kCompute> (rank 0)",
+            "kernel_ms": round(kms, 4),
+        },
+        "parity_sample": {"packets_checked_per_rank": checked, "failures_all_ranks": agg.failures},
+    }
+    tr = pmc_traffic(n, L)
+    if tr is not None:
+        result["roofline"]["traffic"] = tr["traffic_bytes"]
+        result["roofline"]["traffic_source"] = (
+            f"profiles/{PMC_TRAFFIC_FILE}: {tr['kernel']} HBM bytes per launch (FETCH_SIZE x "
+            f"{tr['fetch_correction']} + WRITE_SIZE), {tr['ratio_to_algorithmic']}x the algorithmic bytes")
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        host = d_buf[: min(n, 16384) * L].cpu().numpy()
+        result["cpu_baseline"], result["cpu_context"] = cpu_baseline(orc, host, L, d_out, args)
+
+    if args.extra:
+        result["extra"] = extra_measurements(eng, stream, args, world)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if agg.failures:
+        log(f"bench.py: {agg.failures} ICRC mismatches against the CPU restatement")
+        return 1
+    return 0
+
+
+def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_rank: int):
+    """Rank-local parity: the first and last k packets of this rank's batch against the CPU
+    restatement.  Returns (mismatches, packets checked)."""
+    spans = [(0, min(n, k))]
+    if n > k:
+        spans.append((max(k, n - k), n))
+    fails = checked = 0
+    got_all = d_out.cpu().numpy().view(np.uint32)
+    for a, b in spans:
+        host = d_buf[a * L: b * L].cpu().numpy()
+        off = np.arange(b - a, dtype=np.uint64) * np.uint64(L)
+        want = orc.compute_icrc_batch(host, off, np.full(b - a, L, np.uint32))
+        got = got_all[a:b].copy()
+        if rank == inject_rank:
+            got[0] ^= 1
+        fails += int(np.count_nonzero(got != want))
+        checked += b - a
+    return fails, checked
 
 
 PMC_TRAFFIC_FILE = "r01_pmc_traffic.json"
@@ -73,184 +313,119 @@ def pmc_traffic(n: int, L: int):
     return tr
 
 
-def dev(a: np.ndarray) -> torch.Tensor:
+def _timed_loop(fn, budget: float):
+    """Repeat fn() (returns (seconds, ...)) until `budget` seconds of measured time."""
+    secs, passes, last = 0.0, 0, None
+    while secs < budget or passes == 0:
+        last = fn()
+        secs += last[0]
+        passes += 1
+    return secs, passes, last
+
+
+def cpu_baseline(orc, host, L: int, d_out, args):
+    """cpu_baseline: compute_icrc with the crc32fast-1.4.2-equivalent PCLMULQDQ core on one core
+    over a bounded sample of the same packets.  cpu_context, beside it: the same on
+    every core of this job's CPU share (the box caps a job at 16; os.cpu_count() reports the whole
+    machine); the verify leg (is_icrc_valid, with and without the trailer zeroing); the emulator's
+    per-packet send path (8 KiB alloc + memset, copy in, CRC, copy out: net/util.rs:172-186,
+    packet_processor.rs:210-265); and configs[0] as stated — one QP's 64 x 4156-B WRITE (256 KiB,
+    FIRST + 62 MIDDLE + LAST), compute on send then verify with zeroing on receive, per packet."""
+    cs = host.size // L
+    got = d_out[:cs].cpu().numpy().view(np.uint32)
+    secs, passes, last = _timed_loop(lambda: orc.fast_icrc_strided_timed(host, L, L, cs, threads=1), args.cpu_seconds)
+    cpu_ok = bool(np.array_equal(last[1], got))
+    base = {
+        "value": round(cs * L * passes / secs / GIB, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{cs} x {L}-B packets of the same batch, {passes} passes, {secs:.1f} s; compute_icrc "
+                  f"with a crc32fast-1.4.2-equivalent PCLMULQDQ core (oracle/icrc_fast.c); matches GPU: {cpu_ok}",
+    }
+    threads = max(1, min(16, os.cpu_count() or 1))
+    budget = args.cpu_seconds / 5
+    ctx = {}
+
+    def rate(fn, nbytes):
+        s, p, last = _timed_loop(fn, budget)
+        return round(nbytes * p / s / GIB, 3), round(s, 2), last
+
+    g, s, _ = rate(lambda: orc.fast_icrc_strided_timed(host, L, L, cs, threads=threads), cs * L)
+    ctx["compute_all_cores"] = {"GiB/s": g, "cores": threads, "seconds": s}
+    vbuf = host.copy()
+    orc_out = orc.fast_icrc_strided_timed(host, L, L, cs, threads=threads)[1]
+    vbuf.reshape(cs, L)[:, L - 4:] = orc_out.view(np.uint8).reshape(cs, 4)  # trailers written
+    for name, th in (("verify_1_core", 1), ("verify_all_cores", threads)):
+        g, s, last = rate(lambda th=th: orc.fast_verify_strided_timed(vbuf, L, L, cs, threads=th, zero=False), cs * L)
+        ctx[name] = {"GiB/s": g, "cores": th, "seconds": s, "all_ok": bool(last[1].all())}
+    zb = vbuf.copy()
+    s0, ok0 = orc.fast_verify_strided_timed(zb, L, L, cs, threads=1, zero=True)
+    ctx["verify_zero_trailer_1_core"] = {"GiB/s": round(cs * L / s0 / GIB, 3), "cores": 1, "seconds": round(s0, 2),
+                                         "all_ok": bool(ok0.all()), "note": "one pass (the zeroing is destructive)"}
+    g, s, _ = rate(lambda: orc.fast_emulator_path_timed(host, L, L, cs), cs * L)
+    ctx["emulator_send_path_1_core"] = {"GiB/s": g, "cores": 1, "seconds": s}
+    c0buf, c0off, c0len = orc.synth_write(256 << 10, 4096, local_va=0x7F7E8EE00000, remote_va=0x7F7E8FC00000,
+                                          rkey=0x2000003, dqpn=2, psn0=0, msn=0, dst_ip=0xC0A80003,
+                                          payload_key=0xC0)
+    c0bytes = int(c0len.astype(np.uint64).sum())
+    for name, th in (("c0_roundtrip_1_core", 1), ("c0_roundtrip_all_cores", threads)):
+        reps = 50
+        s, p, last = _timed_loop(lambda th=th: orc.fast_c0_roundtrip_timed(c0buf, c0off, c0len, threads=th, reps=reps),
+                                 budget)
+        ctx[name] = {"GiB/s": round(c0bytes * reps * th * p / s / GIB, 3), "cores": th, "seconds": round(s, 2),
+                     "packets_per_message": int(c0len.size), "failed_verifies": last[1],
+                     "what": "configs[0]: 64 x 4156-B WRITE, emulator send path + is_icrc_valid (zeroing) per packet"}
+    return base, ctx
+
+
+# ---- secondary configs -----------------------------------------------------------------------
+def dev(a: np.ndarray):
+    import torch
+
     return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
 
 
-def time_kernel(fn, steps: int, warmup: int, world: int):
-    """Warmup, barrier+sync, K timed launches (HIP events on the current stream), sync+barrier.
-    Returns (wall seconds, max over ranks; kernel ms per launch from events)."""
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(steps):
-        fn()
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-    return wall, ev0.elapsed_time(ev1) / steps
-
-
-def main() -> int:
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    import icrc_amd
-    from icrc_amd import workloads
-
-    eng = icrc_amd.Engine(local)
-    stream = torch.cuda.current_stream().cuda_stream
-
-    # ---- C1 workload: one QP stream per rank (dqpn = 2 + rank, distinct payload seed) ----
-    n = args.packets
-    w = workloads.write_middle_stream(n, args.pmtu, dqpn=2 + rank, payload_key=0x5EED5EED + rank)
-    L = int(w.lens[0])
-    d_buf = workloads.synthesize(eng, w, stream=stream)
-    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
-
-    def step():
-        eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), False, stream)
-
-    wall, kms = time_kernel(step, args.steps, args.warmup, world)
-    bytes_per_step = n * L
-    value = world * bytes_per_step * args.steps / wall / GIB
-    achieved = bytes_per_step / (kms * 1e-3) / 1e9
-
-    result = {
-        "metric": "device-resident ICRC GiB/s over 4 KiB-MTU packet batches; % of HBM-read roofline",
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (device-synthesised RDMA WRITE_MIDDLE packets, splitmix64 payload)",
-        "config": {
-            "workload": "configs[1]: 1Mi x 4KiB-MTU packets per GPU, device-resident ICRC compute"
-                        + (f" (configs[4]: {world} independent QP streams, one per GPU)" if world > 1 else ""),
-            "packets_per_gpu": n,
-            "packet_bytes": L,
-            "pmtu": args.pmtu,
-            "bytes_per_gpu_per_step": bytes_per_step,
-            "parallelism": f"shard-per-gpu x{world} (no collective)",
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "kernel": "icrc_batch_kernel<kCompute>",
-            "kernel_ms": round(kms, 4),
-        },
-    }
-    tr = pmc_traffic(n, L)
-    if tr is not None:
-        result["roofline"]["traffic"] = tr["traffic_bytes"]
-        result["roofline"]["traffic_source"] = (
-            f"profiles/{PMC_TRAFFIC_FILE}: {tr['kernel']} HBM bytes per launch (FETCH_SIZE x "
-            f"{tr['fetch_correction']} + WRITE_SIZE), {tr['ratio_to_algorithmic']}x the algorithmic bytes")
-
-    # ---- CPU baseline: rank 0, N = 1 only ----
-    parity = True
-    if rank == 0 and world == 1 and not args.no_cpu:
-        import oracle as orc  # the checker / CPU port: used only in this leg
-
-        cs = min(n, 16384)  # 68 MB sample of the same packets
-        host = d_buf[: cs * L].cpu().numpy()
-        secs, passes = 0.0, 0
-        cpu_out = None
-        while secs < args.cpu_seconds or passes == 0:
-            s, cpu_out = orc.fast_icrc_strided_timed(host, L, L, cs, threads=1)
-            secs += s
-            passes += 1
-        cpu_ok = bool(np.array_equal(cpu_out, d_out[:cs].cpu().numpy().view(np.uint32)))
-        parity = cpu_ok
-        result["cpu_baseline"] = {
-            "value": round(cs * L * passes / secs / GIB, 3),
-            "unit": "GiB/s",
-            "cores": 1,
-            "kind": "port",
-            "sample": f"{cs} x {L}-B packets of the same batch, {passes} passes, {secs:.1f} s; "
-                      "compute_icrc with a crc32fast-1.4.2-equivalent PCLMULQDQ core "
-                      f"(oracle/icrc_fast.c); matches GPU: {cpu_ok}",
-        }
-        result["parity_sample_ok"] = cpu_ok
-        result["cpu_context"] = cpu_context(orc, host, L, cs, args.cpu_seconds / 4)
-
-    if args.extra:
-        result["extra"] = extra_measurements(eng, stream, args, world)
-
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return 0 if parity else 1
-
-
-def cpu_context(orc, host, L, cs, budget):
-    """Beside the 1-core cpu_baseline: the same port on every core of this job's CPU
-    share (the box caps a job at 16; os.cpu_count() reports the whole machine), and the emulator's
-    per-packet send path around compute_icrc on one core (8 KiB vec alloc + memset, payload copy
-    in, CRC, UDP-payload copy out: net/util.rs:172-186, packet_processor.rs:210-265)."""
-    threads = max(1, min(16, os.cpu_count() or 1))
-    out = {}
-    for name, fn in (("all_cores", lambda: orc.fast_icrc_strided_timed(host, L, L, cs, threads=threads)),
-                     ("emulator_path_1_core", lambda: orc.fast_emulator_path_timed(host, L, L, cs))):
-        secs, passes = 0.0, 0
-        while secs < budget or passes == 0:
-            s, _ = fn()
-            secs += s
-            passes += 1
-        out[name] = {"GiB/s": round(cs * L * passes / secs / GIB, 3),
-                     "cores": threads if name == "all_cores" else 1, "seconds": round(secs, 2)}
-    return out
-
-
 def extra_measurements(eng, stream, args, world):
-    """Secondary configs: verify pass, mixed MTU (configs[2]), 16 MiB round trip
-    (configs[3]) and the host-resident (PCIe) rate."""
-    import icrc_amd
+    """Secondary configs: verify pass, trailer store / zeroing (the reference's own store
+    semantics), mixed MTU (configs[2]), 16 MiB round trip (configs[3]), the fused send /
+    receive kernels and the host-resident (PCIe) rate."""
+    import torch
+
     from icrc_amd import workloads
 
     ex = {}
-    # verify over the C1 batch with trailers written
     n = args.packets
     w = workloads.write_middle_stream(n, args.pmtu)
     L = int(w.lens[0])
     d_buf = workloads.synthesize(eng, w, stream=stream)
     d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
-    eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), True, stream)
     d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    wall, kms = time_kernel(lambda: eng.verify_strided(d_buf.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream),
-                            args.steps, args.warmup, world)
+
+    def frac(ms, nbytes):
+        return round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+
+    # PacketWriter::write stores the trailer (packet_processor.rs:263): compute + write_trailer
+    _, kms = time_kernel(lambda: eng.compute_strided(d_buf.data_ptr(), L, L, n, d_out.data_ptr(), True, stream),
+                         args.steps, args.warmup, world)
+    ex["compute_c1_write_trailer"] = {"kernel_ms": round(kms, 4), "GiB/s": round(n * L / (kms * 1e-3) / GIB, 1),
+                                      "frac_of_peak": frac(kms, n * L)}
+    # verify over the C1 batch with trailers written
+    _, kms = time_kernel(lambda: eng.verify_strided(d_buf.data_ptr(), L, L, n, d_ok.data_ptr(), False, stream),
+                         args.steps, args.warmup, world)
     ex["verify_c1"] = {"GiB/s": round(n * L / (kms * 1e-3) / GIB, 1), "kernel_ms": round(kms, 4),
-                       "all_ok": bool((d_ok == 1).all().item())}
+                       "frac_of_peak": frac(kms, n * L), "all_ok": bool((d_ok == 1).all().item())}
+    # is_icrc_valid zeroes the trailer (packet_processor.rs:350): the first pass sees the real
+    # trailers (checked), later passes compare against zeros — the same work and traffic
+    eng.verify_strided(d_buf.data_ptr(), L, L, n, d_ok.data_ptr(), True, stream)
+    torch.cuda.synchronize()
+    first_ok = bool((d_ok == 1).all().item())
+    zeroed = bool((d_buf.view(n, L)[:, L - 4:] == 0).all().item())
+    _, kms = time_kernel(lambda: eng.verify_strided(d_buf.data_ptr(), L, L, n, d_ok.data_ptr(), True, stream),
+                         args.steps, args.warmup, world)
+    ex["verify_c1_zero_trailer"] = {"kernel_ms": round(kms, 4), "GiB/s": round(n * L / (kms * 1e-3) / GIB, 1),
+                                    "frac_of_peak": frac(kms, n * L), "first_pass_all_ok": first_ok,
+                                    "trailers_zeroed": zeroed}
     del d_buf, d_out, d_ok
 
     # mixed MTU
@@ -258,15 +433,15 @@ def extra_measurements(eng, stream, args, world):
     d_buf = workloads.synthesize(eng, wm, stream=stream)
     d_off, d_len = dev(wm.off), dev(wm.lens)
     d_out = torch.zeros(wm.n, dtype=torch.int32, device="cuda")
-    wall, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n,
-                                                      d_out.data_ptr(), False, 0, stream),
-                            args.steps, args.warmup, world)
+    _, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n,
+                                                   d_out.data_ptr(), False, 0, stream),
+                         args.steps, args.warmup, world)
     tot = int(wm.lens.astype(np.uint64).sum())
     ex["mixed_mtu_c2"] = {"packets": wm.n, "bytes": tot, "GiB/s": round(tot / (kms * 1e-3) / GIB, 1),
-                          "kernel_ms": round(kms, 4)}
+                          "kernel_ms": round(kms, 4), "frac_of_peak": frac(kms, tot)}
     del d_buf, d_out, d_off, d_len
 
-    # 16 MiB WRITE round trip: compute(send, write trailer) + verify(recv)
+    # 16 MiB WRITE round trip: compute(send, write trailer) + verify(recv, zero trailer)
     w3 = workloads.write_message(16 << 20, 4096)
     d_buf = workloads.synthesize(eng, w3, stream=stream)
     d_off, d_len = dev(w3.off), dev(w3.lens)
@@ -275,9 +450,9 @@ def extra_measurements(eng, stream, args, world):
 
     def rt():
         eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_out.data_ptr(), True, 0, stream)
-        eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), False, 0, stream)
+        eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), True, 0, stream)
 
-    wall, kms = time_kernel(rt, args.steps, args.warmup, world)
+    _, kms = time_kernel(rt, args.steps, args.warmup, world)
     tot3 = int(w3.lens.astype(np.uint64).sum())
     ex["roundtrip_16MiB_c3"] = {"packets": w3.n, "ms_per_roundtrip": round(kms, 4),
                                 "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1),
@@ -285,39 +460,18 @@ def extra_measurements(eng, stream, args, world):
     del d_buf, d_off, d_len, d_out, d_ok
 
     ex.update(fused_send_receive(eng, stream, args, world))
-
-    # host-resident: packets in pinned host memory -> H2D -> kernel -> D2H of ICRCs
-    nh = min(args.packets, 1 << 18)
-    wh = workloads.write_middle_stream(nh, args.pmtu)
-    Lh = int(wh.lens[0])
-    d_buf = workloads.synthesize(eng, wh, stream=stream)
-    h_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, pin_memory=True)
-    h_buf.copy_(d_buf)
-    del d_buf
-    torch.cuda.synchronize()
-    h_np = h_buf.numpy()
-    p_np = h_np.copy()  # pageable copy of the same packets
-    reps = max(3, args.steps // 4)
-    for name, arr in (("pinned", h_np), ("pageable", p_np)):
-        eng.compute_batch_host(arr, wh.off, wh.lens)  # warm (allocates the stages)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            got = eng.compute_batch_host(arr, wh.off, wh.lens)
-        secs = (time.perf_counter() - t0) / reps
-        ex[f"host_resident_{name}"] = {
-            "packets": nh, "GiB/s": round(nh * Lh / secs / GIB, 2), "ms": round(secs * 1e3, 3),
-            "note": "icrc_compute_batch_ex: packets in host memory -> H2D (64 MiB chunks, 2 streams "
-                    "overlapping copy and kernel) -> ICRCs back to host; PCIe Gen5 x16 bound"}
-    ex["host_resident_results_match_device"] = bool(np.array_equal(got, host_icrc_ref(eng, h_np, wh, stream)))
+    ex.update(host_resident(eng, stream, args))
     return ex
 
 
 def fused_send_receive(eng, stream, args, world):
-    """§8f rows 1-3 at C1 scale: the fused send packetizer turning 256 x 16 MiB RDMA WRITE
-    messages (1 Mi x 4156-B packets) into wire packets with trailers, then the fused receive
+    """§8f rows 1-3 at C1 scale: the fused send packetizer turning 192 x 16 MiB RDMA WRITE
+    messages (786 K x 4156-B packets) into wire packets with trailers, then the fused receive
     (verify + strip + parse) over the same wire buffer.  Algorithmic HBM bytes per packet:
     send = 4096 payload read + 4156 wire write + 8 result; receive = 4156 read + 72 descriptor
     + 1 ok byte written."""
+    import torch
+
     import icrc_amd
 
     out = {}
@@ -377,14 +531,90 @@ def fused_send_receive(eng, stream, args, world):
     return out
 
 
-def host_icrc_ref(eng, h_np, wh, stream):
-    """Device-resident ICRCs of the same packets (to check the host-resident path)."""
-    d = torch.from_numpy(h_np).cuda()
-    L = int(wh.lens[0])
-    d_out = torch.zeros(wh.n, dtype=torch.int32, device="cuda")
-    eng.compute_strided(d.data_ptr(), L, L, wh.n, d_out.data_ptr(), False, stream)
+def host_resident(eng, stream, args):
+    """Packets in host memory (pinned and pageable) -> H2D -> kernel -> ICRCs back (PCIe bound;
+    never the headline value)."""
+    import torch
+
+    from icrc_amd import workloads
+
+    ex = {}
+    nh = min(args.packets, 1 << 18)
+    wh = workloads.write_middle_stream(nh, args.pmtu)
+    Lh = int(wh.lens[0])
+    d_buf = workloads.synthesize(eng, wh, stream=stream)
+    h_buf = torch.empty(wh.total_bytes, dtype=torch.uint8, pin_memory=True)
+    h_buf.copy_(d_buf)
     torch.cuda.synchronize()
-    return d_out.cpu().numpy().view(np.uint32)
+    d_ref = torch.zeros(wh.n, dtype=torch.int32, device="cuda")
+    eng.compute_strided(d_buf.data_ptr(), Lh, Lh, wh.n, d_ref.data_ptr(), False, stream)
+    torch.cuda.synchronize()
+    ref = d_ref.cpu().numpy().view(np.uint32)
+    del d_buf
+    h_np = h_buf.numpy()
+    p_np = h_np.copy()  # pageable copy of the same packets
+    reps = max(3, args.steps // 4)
+    got = None
+    for name, arr in (("pinned", h_np), ("pageable", p_np)):
+        eng.compute_batch_host(arr, wh.off, wh.lens)  # warm (allocates the stages)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = eng.compute_batch_host(arr, wh.off, wh.lens)
+        secs = (time.perf_counter() - t0) / reps
+        ex[f"host_resident_{name}"] = {
+            "packets": nh, "GiB/s": round(nh * Lh / secs / GIB, 2), "ms": round(secs * 1e3, 3),
+            "note": "icrc_compute_batch_ex: packets in host memory -> H2D (64 MiB chunks, 2 streams "
+                    "overlapping copy and kernel) -> ICRCs back to host; PCIe Gen5 x16 bound"}
+    ex["host_resident_results_match_device"] = bool(np.array_equal(got, ref))
+    return ex
+
+
+# ---- CPU stub (tests): the N>1 plumbing without GPUs -------------------------------------------
+def run_cpu_stub(args, rank: int, world: int) -> int:
+    import zlib
+
+    import torch.distributed as dist
+
+    from icrc_amd import shard
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    L = 28 + 28 + args.pmtu + 4
+    if args.scaling == "weak":  # one stream per rank
+        lo, hi, key = 0, args.packets, 0x5EED5EED + rank
+    else:  # one stream, sliced: strong-scaling shards are exactly its packet ranges
+        (lo, hi), key = shard.shard_range(args.packets, rank, world), 0x5EED5EED
+    n = hi - lo
+    buf = np.random.default_rng(key).integers(0, 256, hi * L, dtype=np.uint8)[lo * L:]
+    out = np.zeros(n, dtype=np.uint32)
+
+    def step():  # CPU stand-in for the kernel launch (NOT the ICRC)
+        for i in range(n):
+            out[i] = zlib.crc32(buf[i * L:(i + 1) * L])
+
+    wall, _ = time_steps(step, args.steps, args.warmup, world, lambda: None, dist.barrier if world > 1 else None)
+    want = np.array([zlib.crc32(buf[i * L:(i + 1) * L]) for i in range(n)], dtype=np.uint32)
+    got = out.copy()
+    if rank == args.inject_fault_rank and n:
+        got[0] ^= 1
+    fails = int(np.count_nonzero(got != want))
+    agg = shard.aggregate(n * L * args.steps, wall, fails)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC + " [cpu-stub: plumbing test, not the ICRC]", "value": round(agg.gib_per_s, 6),
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(agg.seconds / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic (cpu stub)",
+            "config": {"workload": "cpu-stub", "packets_per_gpu": n, "packet_bytes": L,
+                       "bytes_total_per_step": agg.total_bytes // args.steps,
+                       "packets_total_per_step": agg.total_bytes // args.steps // L,
+                       "parallelism": f"shard-per-rank x{world} (gloo)"},
+            "parity_sample": {"failures_all_ranks": agg.failures},
+        }), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 1 if agg.failures else 0
 
 
 if __name__ == "__main__":

@@ -67,6 +67,24 @@ def synthesize(engine, w: "Workload", d_buf=None, stream: int = 0, pad: int = 0)
     return d_buf
 
 
+def subset(w: "Workload", lo: int, hi: int) -> "Workload":
+    """Packets [lo, hi) of `w` as a workload of their own, offsets rebased to the first one:
+    the bytes synthesised are exactly those packets' bytes in `w` (strong-scaling shards)."""
+    if not 0 <= lo <= hi <= w.n:
+        raise ValueError("bad packet range")
+    if lo == hi:
+        return Workload(w.name, w.hdr[:0].copy(), w.desc[:0].copy(), w.off[:0].copy(), w.lens[:0].copy(), 0, w.stride)
+    base = np.uint64(w.off[lo])
+    desc = w.desc[lo:hi].copy()
+    desc["offset"] -= base
+    desc["hdr_index"] = np.arange(hi - lo, dtype=np.uint32)
+    off = w.off[lo:hi] - base
+    end = int(off[-1]) + int(w.lens[hi - 1])
+    total = max(end, int(off[-1]) + (w.stride or 0)) if w.stride else (end + 3) // 4 * 4
+    return Workload(f"{w.name}[{lo}:{hi}]", w.hdr[w.desc["hdr_index"][lo:hi]].copy(), desc, off,
+                    w.lens[lo:hi].copy(), total, w.stride)
+
+
 def _pad_cnt(n):
     return (4 - (n % 4)) % 4
 

@@ -207,3 +207,108 @@ double fast_emulator_path_timed(const uint8_t *base, uint64_t stride, uint32_t l
     }
     return now_s() - t0;
 }
+
+/* is_icrc_valid with the fast core (packet_processor.rs:341-353). */
+static int fast_is_icrc_valid(uint8_t *pkt, size_t len, int zero) {
+    uint32_t stored, c;
+    memcpy(&stored, pkt + len - 4, 4);
+    if (zero) memset(pkt + len - 4, 0, 4);
+    fast_compute_icrc(pkt, len, &c);
+    return stored == c;
+}
+
+typedef struct {
+    uint8_t *base;
+    uint64_t stride;
+    uint32_t len;
+    uint64_t lo, hi;
+    uint8_t *ok;
+    int zero;
+} vjob_t;
+
+static void *vworker(void *arg) {
+    vjob_t *j = (vjob_t *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) j->ok[i] = (uint8_t)fast_is_icrc_valid(j->base + i * j->stride, j->len, j->zero);
+    return NULL;
+}
+
+double fast_verify_strided_timed(uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, uint8_t *ok,
+                                 int threads, int zero) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    if (len < 44) return -1.0;
+    pthread_t tid[256];
+    vjob_t jobs[256];
+    double t0 = now_s();
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (vjob_t){base, stride, len, n * (uint64_t)t / (uint64_t)threads, n * (uint64_t)(t + 1) / (uint64_t)threads,
+                           ok, zero};
+        if (threads == 1) vworker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, vworker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    return now_s() - t0;
+}
+
+typedef struct {
+    const uint8_t *base;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t n;
+    int reps;
+    uint64_t bad;
+} c0job_t;
+
+static void *c0worker(void *arg) {
+    c0job_t *j = (c0job_t *)arg;
+    for (int r = 0; r < j->reps; r++) {
+        for (uint64_t i = 0; i < j->n; i++) {
+            const uint8_t *pkt = j->base + j->off[i];
+            const uint32_t L = j->len[i];
+            if (L < 44) { j->bad++; continue; }
+            /* send: generate_payload_from_msg (util.rs:172-186) around PacketWriter::write */
+            uint8_t *data = (uint8_t *)malloc(L);
+            memcpy(data, pkt, L);
+            uint8_t *buf = (uint8_t *)calloc(8192, 1);
+            memcpy(buf, data, L);
+            uint32_t c;
+            fast_compute_icrc(buf, L, &c);
+            memcpy(buf + L - 4, &c, 4);
+            uint8_t *udp = (uint8_t *)malloc(L - 28);
+            memcpy(udp, buf + 28, L - 28);
+            /* receive: the datagram as it arrives (IPv4 header + UDP payload), is_icrc_valid */
+            uint8_t *rx = (uint8_t *)malloc(L);
+            memcpy(rx, buf, 28);
+            memcpy(rx + 28, udp, L - 28);
+            if (!fast_is_icrc_valid(rx, L, 1)) j->bad++;
+            __asm__ __volatile__("" ::"r"(rx) : "memory");
+            free(rx);
+            free(udp);
+            free(buf);
+            free(data);
+        }
+    }
+    return NULL;
+}
+
+double fast_c0_roundtrip_timed(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n,
+                               int threads, int reps, uint64_t *bad) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    c0job_t jobs[256];
+    double t0 = now_s();
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (c0job_t){base, off, len, n, reps, 0};
+        if (threads == 1) c0worker(&jobs[t]);
+        else pthread_create(&tid[t], NULL, c0worker, &jobs[t]);
+    }
+    if (threads > 1)
+        for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    const double secs = now_s() - t0;
+    uint64_t b = 0;
+    for (int t = 0; t < threads; t++) b += jobs[t].bad;
+    if (bad) *bad = b;
+    return secs;
+}

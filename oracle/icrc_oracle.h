@@ -152,6 +152,19 @@ double fast_icrc_strided_timed(const uint8_t *base, uint64_t stride, uint32_t le
  * + payload copy in + ICRC + UDP-payload copy out (to_vec). Returns elapsed seconds. */
 double fast_emulator_path_timed(const uint8_t *base, uint64_t stride, uint32_t len, uint64_t n,
                                 uint32_t *out);
+/* is_icrc_valid (packet_processor.rs:341-353) with the crc32fast-equivalent core over packets
+ * base + i*stride, `threads` POSIX threads: ok[i] = 1/0; zero != 0 zeroes each trailer in place
+ * (line 350) — then the buffer holds zero trailers afterwards.  Returns elapsed seconds. */
+double fast_verify_strided_timed(uint8_t *base, uint64_t stride, uint32_t len, uint64_t n, uint8_t *ok,
+                                 int threads, int zero);
+/* configs[0]: the emulator's compute + verify round trip for packets (off[i], len[i]) of `base`
+ * (one QP's WRITE message), `reps` times per thread on `threads` threads, each thread on its own
+ * copy of the message.  Per packet: the send path of fast_emulator_path_timed (vec![0; 8192],
+ * payload copy in, compute_icrc, trailer store, UDP-payload copy out), then the receive check on
+ * the received bytes (is_icrc_valid with the in-place trailer zeroing).  *bad = packets whose
+ * verify failed (0 expected).  Returns elapsed seconds. */
+double fast_c0_roundtrip_timed(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n,
+                               int threads, int reps, uint64_t *bad);
 
 #ifdef __cplusplus
 }

@@ -140,6 +140,14 @@ def lib() -> ctypes.CDLL:
         L.fast_icrc_strided_timed.restype = ctypes.c_double
         L.fast_emulator_path_timed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p]
         L.fast_emulator_path_timed.restype = ctypes.c_double
+        L.fast_verify_strided_timed.argtypes = [
+            u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p, ctypes.c_int, ctypes.c_int,
+        ]
+        L.fast_verify_strided_timed.restype = ctypes.c_double
+        L.fast_c0_roundtrip_timed.argtypes = [
+            u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+        ]
+        L.fast_c0_roundtrip_timed.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -371,3 +379,23 @@ def fast_emulator_path_timed(base: np.ndarray, stride: int, length: int, n: int)
     out = np.zeros(n, dtype=np.uint32)
     secs = lib().fast_emulator_path_timed(_ptr(base), stride, length, n, _ptr(out))
     return secs, out
+
+
+def fast_verify_strided_timed(base: np.ndarray, stride: int, length: int, n: int, threads: int = 1,
+                              zero: bool = False):
+    """is_icrc_valid over a strided batch (zero=True zeroes the trailers of `base` in place)."""
+    ok = np.zeros(n, dtype=np.uint8)
+    secs = lib().fast_verify_strided_timed(_ptr(base), stride, length, n, _ptr(ok), threads, 1 if zero else 0)
+    return secs, ok
+
+
+def fast_c0_roundtrip_timed(base: np.ndarray, off, lens, threads: int = 1, reps: int = 1):
+    """configs[0]: the emulator's per-packet compute (send) + verify (receive, zeroing) round
+    trip over one message's packets, `reps` times on each of `threads` threads.
+    Returns (seconds, failed verifies)."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    bad = ctypes.c_uint64()
+    secs = lib().fast_c0_roundtrip_timed(_ptr(base), _ptr(off), _ptr(lens), off.size, threads, reps,
+                                         ctypes.byref(bad))
+    return secs, int(bad.value)

@@ -37,10 +37,10 @@ if [ "${PMC:-0}" = 1 ]; then
     timeout -k 10 300 rocprofv3 --pmc $C -d $OUT/pmc_bench_$C -o pmc --output-format csv -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmc_bench_$C.log 2>&1; rc=$?
     tail -1 $OUT/pmc_bench_$C.log; stop_if_fatal $rc "pmc bench $C"
-    if [ -x scripts/membench ]; then
+    if [ -x scripts/_build/membench ]; then
       rm -rf $OUT/pmc_mem_$C
       timeout -k 10 300 rocprofv3 --pmc $C -d $OUT/pmc_mem_$C -o pmc --output-format csv -- \
-        ./scripts/membench > $OUT/pmc_mem_$C.log 2>&1; rc=$?
+        ./scripts/_build/membench > $OUT/pmc_mem_$C.log 2>&1; rc=$?
       tail -1 $OUT/pmc_mem_$C.log; stop_if_fatal $rc "pmc membench $C"
     fi
   done

@@ -58,8 +58,8 @@ def _worker(rank, world, port, q):
         if i in (5, 150, 299):
             p[60] ^= 0x10
         fails += 0 if oracle.is_icrc_valid(p) else 1
-    gibs, secs, tot_fails = aggregate(int(lens[lo:hi].sum()), 0.5 + rank, fails)
-    q.put((rank, lo, hi, icrc.tolist(), gibs, secs, tot_fails))
+    gibs, secs, tot_fails, tot_bytes = aggregate(int(lens[lo:hi].sum()), 0.5 + rank, fails)
+    q.put((rank, lo, hi, icrc.tolist(), gibs, secs, tot_fails, tot_bytes))
     dist.destroy_process_group()
 
 
@@ -85,8 +85,63 @@ def test_gloo_world2_shards_and_aggregates():
         assert r[5] == pytest.approx(1.5)        # max over ranks
         assert r[6] == 3                         # summed failures
         assert r[4] == pytest.approx(int(lens.sum()) / 1.5 / (1 << 30))
+        assert r[7] == int(lens.sum())                # summed bytes
 
 
 def test_aggregate_single_process_identity():
-    g, s, f = aggregate(1 << 30, 2.0, 4)
-    assert g == pytest.approx(0.5) and s == 2.0 and f == 4
+    g, s, f, b = aggregate(1 << 30, 2.0, 4)
+    assert g == pytest.approx(0.5) and s == 2.0 and f == 4 and b == 1 << 30
+
+
+# ---- bench.py's own launcher and aggregation (world 2, gloo, CPU stand-in step) ----------------
+import json  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUB_L = 28 + 28 + 256 + 4  # --pmtu 256
+
+
+def _bench(*extra, env_extra=None):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-stub", "--pmtu", "256",
+                        "--steps", "2", "--warmup", "1", *extra],
+                       capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_launcher_world2_weak():
+    rc, res, err = _bench("--gpus", "2", "--packets", "48")
+    assert rc == 0, err[-2000:]
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    assert res["config"]["bytes_total_per_step"] == 2 * 48 * STUB_L  # summed over both ranks
+    assert res["config"]["packets_per_gpu"] == 48
+    assert res["parity_sample"]["failures_all_ranks"] == 0
+
+
+def test_bench_launcher_world2_strong():
+    rc, res, err = _bench("--gpus", "2", "--packets", "65", "--scaling", "strong")
+    assert rc == 0, err[-2000:]
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong"
+    assert res["config"]["bytes_total_per_step"] == 65 * STUB_L  # a fixed total, split 33 + 32
+    assert res["config"]["packets_per_gpu"] == 33  # rank 0's shard (shard_range)
+
+
+def test_bench_launcher_sums_failures_and_fails():
+    rc, res, err = _bench("--gpus", "2", "--packets", "16", "--inject-fault-rank", "1")
+    assert rc != 0
+    assert res["parity_sample"]["failures_all_ranks"] == 1
+
+
+def test_bench_refuses_world_size_mismatch():
+    rc, res, _ = _bench("--gpus", "2", "--packets", "8", env_extra={"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc == 2 and res is None
+
+
+def test_bench_single_rank_stub():
+    rc, res, err = _bench("--packets", "8")
+    assert rc == 0, err[-2000:]
+    assert res["n_gpus"] == 1 and res["config"]["bytes_total_per_step"] == 8 * STUB_L
