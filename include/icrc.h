@@ -71,12 +71,14 @@ int icrc_engine_device_ordinal(const icrc_engine *engine);
 /* The engine's own non-blocking stream (a hipStream_t), for callers without one. */
 void *icrc_engine_stream(const icrc_engine *engine);
 /* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode): 0 = one packet
- * per wavefront at a time, 1..18 = one packet per wavefront, software-pipelined, 19..21 = four
- * packets per wavefront, 24..30 = eight packets per wavefront, 100 + q (q in 19..30) = the
- * default length-split dispatch with q as its short-packet kernel; -1 = the defaults (16 for
- * uniform strided batches of long packets, 24 for short ones; ragged batches are split by length
- * between 24 and the long-packet kernel).
- * Results are identical. */
+ * per wavefront at a time; 13 / 16 = one packet per wavefront, software-pipelined, one / two CRC
+ * chains per wave; 20 = four packets per wavefront; 24, 25, 26 = eight packets per wavefront;
+ * 100 + q / 200 + q (q in 20, 24, 25, 26) = the default length-split dispatch with q as its
+ * short-packet kernel (200: compacting long-packet walker); 301 = the fused single-pass receive
+ * parse; -1 = the defaults (16 for uniform strided batches of long packets, 24 for short ones;
+ * ragged batches are split by length between 24 and the long-packet kernel).  Results are
+ * identical, except diagnostics 15, 18, 31, 32, 35 (ablations, wrong by design).
+ * Other values: ICRC_EINVAL. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
 int icrc_device_count(void);
@@ -166,6 +168,27 @@ int icrc_rx_parse_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d
                          icrc_rx_desc *d_desc, uint8_t *d_ok, int zero_trailer, uint32_t *d_nerr,
                          void *stream);
 
+/* ---- receive-side auto-ACK (§8a row a5: generate_ack, net/util.rs:134-170) ------------------
+ * From the descriptors of icrc_rx_parse_device, the ACK every receive handler sends
+ * (write_first.rs:35-82 and the ten other message handlers): needed when the packet parsed
+ * (status ICRC_RX_OK), its ICRC verified (icrc_ok == ICRC_VERIFY_OK), it is not an ACK, ack_req
+ * is set, its QP is valid (ctx.flags) and psn == ctx.expected_psn.  The ACK is generate_ack's
+ * 48-byte packet: 192.168.0.3 -> 192.168.0.2, ip_id 1, UDP 4791 -> 4791, BTH {Acknowledge, RC,
+ * pkey, dqpn = peer_qpn, psn = expected_psn}, AETH {Ack, 0x1f, msn = pkey} and its ICRC; with
+ * ICRC_ACK_UDP_PAYLOAD_ONLY the 20-byte UDP payload generate_ack returns (util.rs:167-169).
+ * Slot i is d_out + i * out_stride (out_stride % 4 == 0, d_out 4-byte aligned); d_out_len[i] =
+ * 48 / 20, or 0 when no ACK is due (its slot is not written). */
+typedef struct icrc_ack_ctx {
+    uint32_t peer_qpn;     /* qp_context.peer_qpn() of the packet's QP (dqpn)                */
+    uint32_t expected_psn; /* qp_context.expected_psn() before this packet                    */
+    uint32_t flags;        /* ICRC_ACK_CTX_QP_VALID: the QP exists and is not in error state  */
+} icrc_ack_ctx;
+#define ICRC_ACK_CTX_QP_VALID 0x1u
+#define ICRC_ACK_UDP_PAYLOAD_ONLY 0x1u
+int icrc_ack_from_rx_device(icrc_engine *engine, const icrc_rx_desc *d_desc, const icrc_ack_ctx *d_ctx, uint32_t n,
+                            uint8_t *d_out, uint32_t out_stride, uint32_t *d_out_len, uint32_t flags,
+                            void *stream);
+
 /* ---- batched IPv4 header checksum (§8f row 4) ----------------------------------------------
  * calculate_ipv4_checksum (rust_driver/src/responser.rs:321-338): the one's-complement sum of
  * the ten big-endian 16-bit words of the 20-byte IPv4 header at d_base + off (d_off NULL =>
@@ -205,29 +228,39 @@ int icrc_synth_device(icrc_engine *engine, uint8_t *d_base, const icrc_synth_des
  * goes to d_pkt_len[m.first_packet + s] and its ICRC to d_icrc[m.first_packet + s] (both may
  * be NULL).  Payload bytes come from d_src[m.payload_offset + segment start ...].  The
  * fast path needs (payload_offset - local_va) % 4 == 0 and out_offset, slot_stride % 4 == 0;
- * other messages take a byte-wise path with identical results. */
+ * other messages take a byte-wise path with identical results.  A packet longer than 65535 bytes
+ * (IPv4 total length; PacketWriter::write returns LengthTooLong, packet_processor.rs:226-227) is
+ * not written and reports length 0, like one that does not fit. */
 typedef struct icrc_write_msg {
-    uint64_t local_va;       /* source VA of the payload: drives the first segment length */
+    uint64_t local_va;       /* source VA of the payload: drives the first segment length; read
+                                requests: the secondary RETH va (the local SGE, read.rs:69-73) */
     uint64_t remote_va;      /* RETH va of the first packet */
     uint64_t payload_offset; /* byte offset of the message payload in d_src */
     uint64_t out_offset;     /* byte offset of packet 0 in d_wire */
-    uint32_t total_len;      /* sge.len: bytes to send, drives segmentation */
+    uint32_t total_len;      /* sge.len: bytes to send, drives segmentation (read requests: the
+                                secondary RETH len) */
     uint32_t reth_len;       /* common.total_len: the RETH len of every packet (common.rs:113) */
-    uint32_t pmtu;           /* 256 .. 4096 */
+    uint32_t pmtu;           /* 256 .. 4096 (WRITE / READ RESPONSE) */
     uint32_t rkey;
     uint32_t dqpn;
     uint32_t psn;            /* PSN of packet 0 (wraps at 24 bits) */
     uint32_t src_ip, dst_ip; /* host order; the emulator uses 192.168.0.2 (common.rs:124) */
     uint32_t first_packet;   /* index of packet 0 in the flattened packet arrays */
-    uint32_t npackets;       /* icrc_write_segment_count(local_va, total_len, pmtu) */
+    uint32_t npackets;       /* icrc_write_segment_count(local_va, total_len, pmtu); 1 for a read request */
     uint32_t slot_stride;    /* bytes between consecutive packets of this message */
     uint16_t msn;            /* carried in the BTH pkey field (common.rs:91-92) */
     uint16_t ip_id;          /* generate_payload_from_msg uses 1 (net/util.rs:179) */
-    uint8_t kind;            /* 0 = RDMA WRITE, 1 = RDMA READ RESPONSE */
+    uint8_t kind;            /* ICRC_MSG_* below */
     uint8_t tran_type;       /* RC = 0 */
     uint8_t flags;           /* ICRC_WRITE_* below */
-    uint8_t _pad[5];
+    uint8_t _pad;
+    uint32_t lkey;           /* read requests: the secondary RETH rkey (sge.local_key) */
 } icrc_write_msg; /* 88 bytes */
+#define ICRC_MSG_WRITE 0u         /* Write::handle (write.rs:31-96): WRITE FIRST/MIDDLE/LAST/ONLY  */
+#define ICRC_MSG_READ_RESPONSE 1u /* ReadResponse::handle (read_response.rs:30-95)                 */
+#define ICRC_MSG_READ_REQUEST 2u  /* Read::handle (read.rs:33-89): one 76-byte packet, opcode 0x0C,
+                                     RETH {remote_va, rkey, reth_len} + secondary RETH {local_va,
+                                     lkey, total_len}, no payload                                 */
 /* Fill the IPv4 header checksum (RFC 791, as smoltcp's fill_checksum does when the emulator
  * builds the frame, net_agent.rs:93; calculate_ipv4_checksum, responser.rs:321-338).  The
  * ICRC masks those bytes, so it is the same either way.  Default: 0, as PacketWriter leaves it. */
@@ -235,6 +268,12 @@ typedef struct icrc_write_msg {
 /* Segment on the remote VA (rust_driver: calculate_packet_cnt / get_first_packet_max_length,
  * rust_driver/src/utils.rs:19-33) instead of the local VA (emulator, common.rs:152-176). */
 #define ICRC_WRITE_SEG_BY_REMOTE_VA 0x02u
+/* RdmaMessageMetaCommon::solicited on every packet of the message (BTH byte 1 bit 7, packet.rs:
+ * 104-110); the emulator's own send paths leave it false (common.rs:90, read.rs:47). */
+#define ICRC_WRITE_SOLICITED 0x04u
+/* Read requests: ack_req (the request is IbvSendSignaled, read.rs:37).  WRITE / READ RESPONSE
+ * packets carry ack_req on their LAST / ONLY packet regardless (write.rs:41-90). */
+#define ICRC_WRITE_ACK_REQ 0x08u
 /* Number of packets generate_segments_from_request yields (common.rs:152-176) for a message
  * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_SEG_BY_REMOTE_VA);
  * 0 if pmtu == 0. */

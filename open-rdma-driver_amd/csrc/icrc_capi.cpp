@@ -461,12 +461,10 @@ int icrc_engine_default(int device, icrc_engine **out) {
 int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : ICRC_EINVAL; }
 
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
-    const bool hybrid = (variant >= icrc::kHybridVariantBase + icrc::kFirstQuadVariant &&
-                         variant <= icrc::kHybridVariantBase + icrc::kMaxVariant) ||
-                        (variant >= icrc::kHybridCompactBase + icrc::kFirstQuadVariant &&
-                         variant <= icrc::kHybridCompactBase + icrc::kMaxVariant);
-    const bool rx = variant >= icrc::kRxVariantBase && variant <= icrc::kRxVariantBase + icrc::kMaxRxVariant;
-    if (!e || variant < -1 || (variant > icrc::kMaxVariant && !hybrid && !rx)) return ICRC_EINVAL;
+    const bool hybrid = icrc::is_short_variant(variant - icrc::kHybridVariantBase) ||
+                        icrc::is_short_variant(variant - icrc::kHybridCompactBase);
+    const bool rx = variant == icrc::kRxVariantBase + 1;
+    if (!e || (variant != -1 && !icrc::is_batch_variant(variant) && !hybrid && !rx)) return ICRC_EINVAL;
     e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;
 }
@@ -605,6 +603,18 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     if (rc == ICRC_OK) rc = icrc::launch_rx_desc(p, e->num_cu, stream);
     if (scratch && hipFreeAsync(scratch, s) != hipSuccess && rc == ICRC_OK) rc = ICRC_EDEVICE;
     return rc;
+}
+
+int icrc_ack_from_rx_device(icrc_engine *e, const icrc_rx_desc *d_desc, const icrc_ack_ctx *d_ctx, uint32_t n,
+                            uint8_t *d_out, uint32_t out_stride, uint32_t *d_out_len, uint32_t flags, void *stream) {
+    if (n == 0) return ICRC_OK;
+    const uint32_t need = (flags & ICRC_ACK_UDP_PAYLOAD_ONLY) ? 20u : 48u;
+    if (!e || !d_desc || !d_ctx || !d_out || out_stride < need || out_stride % 4 != 0 ||
+        reinterpret_cast<uintptr_t>(d_out) % 4 != 0 || (flags & ~ICRC_ACK_UDP_PAYLOAD_ONLY) != 0)
+        return ICRC_EINVAL;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    return icrc::launch_ack(d_desc, d_ctx, n, d_out, out_stride, d_out_len, flags, e->num_cu, stream);
 }
 
 int icrc_ipv4_checksum_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off, uint64_t stride, uint32_t n,

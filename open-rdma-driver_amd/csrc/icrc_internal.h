@@ -52,19 +52,27 @@ struct BatchParams {
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
-constexpr int kFirstQuadVariant = 19;  // 19..21: 4 packets per wavefront (chunk pipeline, K x D)
 constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
-// Hybrid dispatch threshold: shorter packets go to the quad kernel (per-packet costs / 4), longer
+// Hybrid dispatch threshold: shorter packets go to the oct kernel (per-packet costs / 8), longer
 // ones to the one-packet pipeline (one contiguous row per wave instruction streams faster).
 constexpr uint32_t kSplitLen = 2048;
 // 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
 constexpr int kHybridVariantBase = 100;
-// 200 + q: the same with the compacting long-packet walker (A/B); 300 + r: receive-parse variant r
-// (0 two-pass default, 1 fused S = 2, 2 fused S = 1 D = 2, 3 fused diagnostic).
+// 200 + q: the same with the compacting long-packet walker (A/B); 301: the fused single-pass
+// receive parse (A/B against the two-pass default).
 constexpr int kHybridCompactBase = 200;
 constexpr int kRxVariantBase = 300;
-constexpr int kMaxRxVariant = 3;  // 3: diagnostic (raw header words, wrong descriptors by design)
-constexpr int kMaxVariant = 38;  // 22, 23, 31-38: quad / oct ablations and probes (wrong results by design)
+// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35 are
+// diagnostics whose results are wrong by design.
+inline bool is_batch_variant(int v) {
+    switch (v) {
+    case 0: case 13: case 15: case 16: case 18: case 20: case 24: case 25: case 26: case 31: case 32: case 35:
+        return true;
+    default:
+        return false;
+    }
+}
+inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26; }
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 
@@ -96,6 +104,8 @@ struct PacketizeParams {
     const uint32_t *table;
 };
 int launch_packetize(const PacketizeParams &p, int grid, void *stream);
+int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, uint8_t *out, uint32_t stride,
+               uint32_t *out_len, uint32_t mode, int num_cu, void *stream);
 int launch_ipv4_checksum(uint8_t *base, const uint64_t *off, uint64_t stride, uint32_t n, uint16_t *csum, int fill,
                          void *stream);
 

@@ -119,23 +119,49 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 constexpr int abl_mode(int abl) { return abl & 3; }
 constexpr int abl_aux(int abl) { return abl >> 2; }
 
-template <int ABL>
-__device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[kRows]) {
+// Verify also loads the packet's stored trailer (all lanes, one dword) as load kRows of the same
+// ring position, so that the comparison needs no load of its own after the CRC (a load issued
+// there is the youngest in flight and its wait drains the ring).
+template <int MODE>
+constexpr int ring_words() { return MODE == kVerify ? kRows + 1 : kRows; }
+
+template <int ABL, int MODE>
+__device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[ring_words<MODE>()]) {
     if constexpr (abl_mode(ABL) == 2) {
 #pragma unroll
-        for (int j = 0; j < kRows; ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
+        for (int j = 0; j < ring_words<MODE>(); ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
         return;
     }
     constexpr int kAux = abl_aux(ABL);
-    const int nrec = m.kind == 1 ? static_cast<int>(m.L - 4u) : 0;
+    // compute reads [0, L-4); verify also the trailer [L-4, L) (rows never reach it)
+    const int nrec = m.kind == 1 ? static_cast<int>(MODE == kVerify ? m.L : m.L - 4u) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
     const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
-    // Always kRows loads, no branch: hipcc's static vmcnt accounting takes the minimum over
+    // Always the same loads, no branch: hipcc's static vmcnt accounting takes the minimum over
     // all paths, so a conditional load block anywhere in the ring turns the waits for the
     // current packet into vmcnt(0) and drains the prefetch of the next one.
 #pragma unroll
     for (int j = 0; j < kRows; ++j)
         u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, kAux);
+    if constexpr (MODE == kVerify)
+        u[kRows] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(m.L - 4u), 0, kAux);
+}
+
+// Result of a regular packet of the pipelined path, from registers only: compute -> the ICRC;
+// verify -> OK / MISMATCH against the trailer word loaded with the rows.  TRAILER: the one
+// trailer store of the packet (compute: the ICRC, PacketWriter::write, packet_processor.rs:263;
+// verify: zeros, is_icrc_valid, 350) as a buffer store that every lane issues, lane 0 in range
+// (no branch, so the ring's vmcnt accounting stays exact; an empty slot's descriptor has size 0).
+template <int MODE, bool TRAILER>
+__device__ __forceinline__ uint32_t regular_result(const SlotMeta &m, uint32_t crc, uint32_t stored, uint32_t lane) {
+    if constexpr (TRAILER) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, m.kind == 1 ? static_cast<int>(m.L) : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs,
+                                              static_cast<int>(lane == 0 ? m.L - 4u : 0x80000000u), 0, 0);
+    }
+    if constexpr (MODE == kCompute) return crc;
+    else return stored == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -246,11 +272,12 @@ __device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row
 
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
 // the wave's result buffer.
-// PARSE: 0 off; 1 receive parse (rx_store); 3 diagnostic: the raw header words stored, no decode.
-template <int MODE, int S, int ABL, int PARSE = 0>
+// PARSE: 0 off; 1 receive parse (rx_store).
+template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                            uint32_t lane, const SlotMeta (&m)[S], uint32_t (&u)[S][kRows],
-                                            uint32_t q0, ResultBuf &rb, uint32_t lo = 0) {
+                                            uint32_t lane, const SlotMeta (&m)[S],
+                                            uint32_t (&u)[S][ring_words<MODE>()], uint32_t q0, ResultBuf &rb,
+                                            uint32_t lo = 0) {
     int rmax = 0;
     bool same = true;  // every slot regular with the same row count (the common case)
 #pragma unroll
@@ -313,16 +340,15 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 #pragma unroll
         for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
 #pragma unroll
-        for (int s = 0; s < S; ++s)
+        for (int s = 0; s < S; ++s) {
+            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]),
+                                                             MODE == kVerify ? u[s][ring_words<MODE>() - 1] : 0u, lane);
             if (m[s].kind == 1) {
-                const uint32_t r = packet_result<MODE>(p, m[s].pkt, m[s].L - 4u, ~wave_xor(fin[s]), true, lane);
                 rb_put(rb, q0 + s, r);
-                if constexpr (PARSE == 3) {
-                    if (lane < 18u) reinterpret_cast<uint32_t *>(p.rx + lo + q0 + s)[lane] = hdr[s] ^ r;
-                } else if constexpr (PARSE) {
+                if constexpr (PARSE)
                     rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
-                }
             }
+        }
     }
 #pragma unroll
     for (int s = 0; s < S; ++s)
@@ -340,7 +366,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
 // processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
 // ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
-template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false>
+template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false, bool TRAILER = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -355,14 +381,14 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     rb.v = 0;
     rb.valid = 0;
     SlotMeta m[B][S];
-    uint32_t u[B][S][kRows];
+    uint32_t u[B][S][ring_words<MODE>()];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         if (static_cast<uint32_t>(d) < nsets) {
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 slot_meta<LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
-                slot_load<ABL>(m[d][s], lane, u[d][s]);
+                slot_load<ABL, MODE>(m[d][s], lane, u[d][s]);
             }
         }
     }
@@ -377,10 +403,10 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 slot_meta<LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
-                slot_load<ABL>(m[bp][s], lane, u[bp][s]);
+                slot_load<ABL, MODE>(m[bp][s], lane, u[bp][s]);
             }
             const uint32_t q0 = ts * S;
-            process_set<MODE, S, ABL, PARSE>(p, lds, c, lane, m[b], u[b], q0, rb, lo);
+            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, lo);
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             return true;
@@ -396,7 +422,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 // streams from HBM at ~6.2 TB/s, while four packets per instruction stop at ~4.5 TB/s
 // (profiles/r01_membench.json, patterns D and E).  The walk skips short packets with the
 // ballot of each 64-packet meta block; results are kept per block and stored 64 at a time.
-template <int MODE, int D, int ABL>
+template <int MODE, int D, int ABL, bool TRAILER>
 __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
                                                    uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -412,7 +438,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     int rb_block = -1;
     SlotMeta m[B][1];
     uint32_t qs[B];
-    uint32_t u[B][1][kRows];
+    uint32_t u[B][1][ring_words<MODE>()];
     int inflight = 0;
 
     auto next = [&](SlotMeta &sm, uint32_t &q) __attribute__((always_inline)) {
@@ -457,7 +483,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         next(m[d][0], qs[d]);
-        slot_load<ABL>(m[d][0], lane, u[d][0]);
+        slot_load<ABL, MODE>(m[d][0], lane, u[d][0]);
         if (m[d][0].kind) inflight += 1;
     }
     for (;;) {
@@ -465,7 +491,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
             constexpr int b = decltype(bc)::value;
             constexpr int bp = (b + D) % B;
             next(m[bp][0], qs[bp]);
-            slot_load<ABL>(m[bp][0], lane, u[bp][0]);
+            slot_load<ABL, MODE>(m[bp][0], lane, u[bp][0]);
             if (m[bp][0].kind) inflight += 1;
             if (m[b][0].kind) {
                 const int blk = static_cast<int>(qs[b] >> 6);
@@ -473,7 +499,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
                     if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
                     rb_block = blk;
                 }
-                process_set<MODE, 1, ABL>(p, lds, c, lane, m[b], u[b], qs[b], rb, lo);
+                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, lo);
                 inflight -= 1;
             }
             return true;
@@ -488,7 +514,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
 // batch it runs at the strided rate (1 Mi x 4156 B: 0.75 ms split vs 0.80-0.87 with the walker) —
 // and the compacting S = 1 walker above when they are sparse (on a mixed-MTU batch the dense walk
 // costs 1.32 ms against 0.49).  COMPACT = true: the walker always (A/B: variant 200 + q).
-template <int MODE, bool COMPACT>
+template <int MODE, bool COMPACT, bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -510,7 +536,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
     if constexpr (COMPACT) {
-        run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
+        run_pipelined_long<MODE, 1, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
     } else {
         // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
         // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
@@ -519,216 +545,9 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true>(p, lds, c, lane, lo, nq);
+            run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
         else
-            run_pipelined_long<MODE, 1, kStreamAux << 2>(p, lds, c, lane, lo, nq);
-    }
-}
-
-// ---- row-stream path ------------------------------------------------------------------------
-// A wave's chunk is one flat sequence of 256-byte rows (the sum of R over its regular packets,
-// in packet order).  A ring of RD row loads stays in flight (RD * 256 B per wave); the
-// process side consumes rows in the same order, restarting the Horner accumulator at each
-// packet's first row and finalising at its last.  A short packet costs only its own rows,
-// a long one needs no special path, and every ring load is unconditional (exact vmcnt
-// accounting).  Misaligned packets and L % 4 != 0 are skipped by the stream and done by a
-// tail loop; L < 44 packets are recorded as errors when the process cursor passes them.
-struct RowCursor {  // wave-uniform
-    uint32_t q;     // packet sequence number within the chunk
-    int j;          // row within the packet
-    int R;          // rows of the current packet (0 = past the end)
-    int k0;
-    uint8_t *pkt;
-    uint32_t L;
-};
-
-// R >= 1: regular packet; 0: L < 44 (error); -1: irregular (generic path).
-__device__ __forceinline__ int classify(const uint8_t *pkt, uint32_t L, int &k0) {
-    if (L < ICRC_MIN_PACKET) return 0;
-    if (((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) != 0) return -1;
-    const int N = 1 + static_cast<int>((L - 4u) >> 2);
-    const int R = (N + 63) >> 6;
-    k0 = N - 64 * R;
-    return R;
-}
-
-__device__ __forceinline__ void meta_read(const MetaBlock &mb, uint32_t q, uint64_t &off, uint32_t &L) {
-    const int l = static_cast<int>(q & 63u);
-    off = meta_off(mb, l);
-    L = readlane_u32(mb.len, l);
-}
-
-// Result buffer keyed by 64-packet block: switching block flushes the previous one.
-template <int MODE>
-__device__ __forceinline__ void rb_record(const BatchParams &p, ResultBuf &rb, int &rb_block, uint32_t lo,
-                                          uint32_t q, uint32_t r, uint32_t lane) {
-    const int blk = static_cast<int>(q >> 6);
-    if (blk != rb_block) {
-        if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
-        rb_block = blk;
-    }
-    rb_put(rb, q, r);
-}
-
-template <int MODE, int RD, bool PARSE = false>
-__device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                              uint32_t lane, uint32_t lo, uint32_t nq) {
-    if (nq == 0) return;
-    const bool ragged = p.off != nullptr || p.len != nullptr;
-    MetaBlock ml, mprev;  // load-side block and the one before it (the process side lags)
-    ml.block = mprev.block = -1;
-    ml.off_lo = ml.off_hi = ml.len = 0;
-    mprev.off_lo = mprev.off_hi = mprev.len = 0;
-    bool irregular = false;
-    ResultBuf rb;
-    rb.v = 0;
-    rb.valid = 0;
-    int rb_block = -1;
-
-    auto meta_at = [&](uint32_t q, bool load_side, uint64_t &off, uint32_t &L) __attribute__((always_inline)) {
-        if (!ragged) {
-            off = static_cast<uint64_t>(lo + q) * p.stride;
-            L = p.ulen;
-            return;
-        }
-        const int blk = static_cast<int>(q >> 6);
-        if (load_side) {
-            if (blk != ml.block) {
-                mprev = ml;
-                meta_fetch(p, ml, lo, lo + nq, blk, lane);
-            }
-            meta_read(ml, q, off, L);
-        } else if (blk == ml.block) {
-            meta_read(ml, q, off, L);
-        } else if (blk == mprev.block) {
-            meta_read(mprev, q, off, L);
-        } else {  // only after a long run of skipped packets
-            MetaBlock t;
-            meta_fetch(p, t, lo, lo + nq, blk, lane);
-            meta_read(t, q, off, L);
-        }
-    };
-
-    // Advance a cursor to the next packet that has rows.  The process side also records
-    // L < 44 packets as errors and notes irregular ones for the tail loop.
-    auto next_packet = [&](RowCursor &cur, bool load_side) __attribute__((always_inline)) {
-        for (;;) {
-            cur.q += 1u;
-            if (cur.q >= nq) {
-                cur.R = 0;
-                cur.pkt = p.base;
-                cur.L = 0;
-                cur.k0 = 0;
-                cur.j = 0;
-                return;
-            }
-            uint64_t off;
-            uint32_t L;
-            meta_at(cur.q, load_side, off, L);
-            uint8_t *pkt = p.base + off;
-            int k0 = 0;
-            const int R = classify(pkt, L, k0);
-            if (R > 0) {
-                cur.R = R;
-                cur.k0 = k0;
-                cur.pkt = pkt;
-                cur.L = L;
-                cur.j = 0;
-                return;
-            }
-            if (!load_side) {
-                if (R < 0) {
-                    irregular = true;
-                } else {
-                    if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
-                    rb_record<MODE>(p, rb, rb_block, lo, cur.q, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN, lane);
-                    if constexpr (PARSE) rx_store(p.rx, lo + cur.q, 0u, off, L, ICRC_VERIFY_BADLEN, lane, c);
-                }
-            }
-        }
-    };
-
-    RowCursor lc, pc;
-    lc.q = pc.q = 0xFFFFFFFFu;
-    next_packet(lc, true);
-    next_packet(pc, false);
-
-    // one row load per ring slot; past the end the descriptor has zero size (load -> 0)
-    auto load_row = [&](uint32_t &dst) __attribute__((always_inline)) {
-        const int nrec = lc.R > 0 ? static_cast<int>(lc.L - 4u) : 0;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(lc.pkt, 0, nrec, 0x00020000);
-        const uint32_t voff = 4u * static_cast<uint32_t>(lc.k0 - 1 + static_cast<int>(lane)) + 256u * static_cast<uint32_t>(lc.j);
-        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, kStreamAux);
-        if (lc.R > 0) {
-            lc.j += 1;
-            if (lc.j == lc.R) next_packet(lc, true);
-        }
-    };
-
-    uint32_t ring[RD];
-    static_for<RD>([&](auto ic) __attribute__((always_inline)) -> bool {
-        load_row(ring[decltype(ic)::value]);
-        return true;
-    });
-
-    uint32_t acc = 0;
-    uint32_t hdr = 0;  // PARSE: packet word w in lane w (w < 18), gathered from rows 0 and 1
-    while (pc.R > 0) {
-        static_for<RD>([&](auto ic) __attribute__((always_inline)) -> bool {
-            constexpr int i = decltype(ic)::value;
-            if (pc.R == 0) return false;
-            uint32_t u = ring[i];
-            if constexpr (PARSE) {
-                if (pc.j < 2) {
-                    const int sl = static_cast<int>(lane) + 1 - pc.k0 - 64 * pc.j;  // lane holding word `lane`
-                    const uint32_t v = static_cast<uint32_t>(
-                        __builtin_amdgcn_ds_bpermute((sl & 63) << 2, static_cast<int>(u)));
-                    hdr = (sl >= 0 && sl < 64) ? v : (pc.j == 0 ? 0u : hdr);
-                }
-            }
-            if (pc.j < 2) u |= head_mask(pc.k0 + static_cast<int>(lane) + 64 * pc.j);
-            if (pc.j == 0) acc = u;
-            else acc = step_m64(lds, acc, u, c);
-            pc.j += 1;
-            if (pc.j == pc.R) {
-                const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
-                const uint32_t r = packet_result<MODE>(p, pc.pkt, pc.L - 4u, crc, true, lane);
-                rb_record<MODE>(p, rb, rb_block, lo, pc.q, r, lane);
-                if constexpr (PARSE)
-                    rx_store(p.rx, lo + pc.q, hdr, static_cast<uint64_t>(pc.pkt - p.base), pc.L, r, lane, c);
-                next_packet(pc, false);
-            }
-            load_row(ring[i]);
-            return true;
-        });
-    }
-    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
-
-    if (irregular) {  // misaligned packets / L % 4 != 0: the generic per-packet path
-        MetaBlock t;
-        t.block = -1;
-        t.off_lo = t.off_hi = t.len = 0;
-        for (uint32_t q = 0; q < nq; ++q) {
-            uint64_t off;
-            uint32_t L;
-            if (!ragged) {
-                off = static_cast<uint64_t>(lo + q) * p.stride;
-                L = p.ulen;
-            } else {
-                const int blk = static_cast<int>(q >> 6);
-                if (blk != t.block) meta_fetch(p, t, lo, lo + nq, blk, lane);
-                meta_read(t, q, off, L);
-            }
-            uint8_t *pkt = p.base + off;
-            int k0 = 0;
-            if (classify(pkt, L, k0) < 0) {
-                uint32_t hdr_slow = 0;
-                if constexpr (PARSE) hdr_slow = rx_header_bytes(pkt, L, lane);  // before the trailer is zeroed
-                const uint32_t r = handle_packet<MODE>(p, pkt, L, lds, c, lane);
-                if (lane == 0) store_result<MODE>(p, lo + q, r);
-                if constexpr (PARSE) rx_store(p.rx, lo + q, hdr_slow, off, L, r, lane, c);
-            }
-        }
+            run_pipelined_long<MODE, 1, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
     }
 }
 
@@ -736,8 +555,8 @@ __device__ __forceinline__ void run_rowstream(const BatchParams &p, const char *
 //   0            one packet per wave at a time, no pipelining, strided packet assignment
 //   S, D, ABL    pipelined with S chains and a D-deep ring over a contiguous packet chunk per
 //                wave; ABL = 0 (real), 1 (loads only, no CRC: a memory-pipeline bound),
-//                2 (CRC only, no loads: a compute bound).
-template <int MODE, int S, int D, int ABL>
+//                2 (CRC only, no loads: a compute bound); TRAILER: write / zero the trailers.
+template <int MODE, int S, int D, int ABL, bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -755,14 +574,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
-    if constexpr (S < 0) {
-        const uint32_t chunk = wave_chunk(p.n, tw);
-        const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
-        if (lo64 >= p.n) return;
-        const uint32_t lo = static_cast<uint32_t>(lo64);
-        const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-        run_rowstream<MODE, -S>(p, lds, c, lane, lo, nq);
-    } else if constexpr (S == 0) {
+    if constexpr (S == 0) {
         for (uint32_t i = gw; i < p.n; i += tw) {
             const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
             const uint32_t L = p.len ? p.len[i] : p.ulen;
@@ -776,13 +588,13 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
         if (lo64 >= p.n) return;
         const uint32_t lo = static_cast<uint32_t>(lo64);
         const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-        run_pipelined<MODE, S, D, ABL>(p, lds, c, lane, lo, nq);
+        run_pipelined<MODE, S, D, ABL, 0, false, TRAILER>(p, lds, c, lane, lo, nq);
     }
 }
 
 // Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
 // words gathered from each packet's first two rows.
-template <int S, int D, int PARSE = 1>
+template <int S, int D, bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -804,7 +616,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, S, D, kStreamAux << 2, PARSE>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, S, D, kStreamAux << 2, 1, false, TRAILER>(p, lds, c, lane, lo, nq);
 }
 
 // ---- receive parse, pass 2 (icrc_rx_parse_device default) ----------------------------------
@@ -924,27 +736,31 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
     }
 }
 
-// ---- fused send packetizer (WRITE / READ RESPONSE messages) -----------------------------------
-// One wavefront per packet, the same row-stream ring as above, but a "row" is built rather
-// than read: header words come from the message descriptor (computed on the scalar unit,
-// placed per lane by selects), payload words from the memory-region buffer (one coalesced
-// buffer_load_dword per lane per row).  Each word is stored to the wire buffer and folded into
-// the ICRC in the same step; the ICRC is the trailer.  Byte-identical to PacketWriter::write.
+// ---- fused send packetizer (WRITE / READ RESPONSE / READ REQUEST messages) ---------------------
+// One wavefront per packet.  A wave owns a contiguous range of packets and walks it with the C1
+// ring (one packet per slot, the next slot's payload rows in flight while a packet is processed).
+// Every slot is kRows (17) rows of 64 words, END-aligned: the packet occupies the last R rows and
+// the rows before it are leading zeros (loads out of range -> 0, stores out of range -> dropped,
+// a zero accumulator stays zero), so every slot issues the same 17 loads and 17 stores, with no
+// branch on the packet's length: the compiler's vmcnt accounting stays exact.  Header words are
+// built on the scalar unit when the slot is filled (one VGPR per slot: header word w in lane w),
+// payload words come from the memory-region buffer, each word is stored to the wire buffer and
+// folded into the ICRC in the same step, and the ICRC is the trailer.  Byte-identical to
+// PacketWriter::write.  Packets whose payload or slot is not 4-byte aligned take a byte-wise loop
+// after the ring; packets that do not fit report length 0.
 
-struct PacketHdr {  // wave-uniform; words are the LE u32 of header bytes 4w .. 4w+3
-    uint32_t w[14];
+// icrc_write_msg dword offsets
+enum : int {
+    kMLocalVa = 0, kMRemoteVa = 2, kMPayloadOff = 4, kMOutOff = 6, kMTotal = 8, kMRethLen = 9, kMPmtu = 10,
+    kMRkey = 11, kMDqpn = 12, kMPsn = 13, kMSrcIp = 14, kMDstIp = 15, kMFirst = 16, kMNpk = 17, kMSlot = 18,
+    kMMsnId = 19, kMKind = 20, kMLkey = 21, kMsgDwords = 22
 };
-
-// Segment s of a message (generate_segments_from_request + Write::handle / ReadResponse::handle)
-struct SegInfo {
-    uint32_t start, len, L, pad;
-    uint64_t out;       // packet offset in d_wire
-    uint64_t src;       // payload offset in d_src
-    int R, k0;
-};
+static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout");
+static_assert(offsetof(icrc_write_msg, lkey) == 4 * kMLkey, "icrc_write_msg layout");
+constexpr uint32_t kSendOOR = 0x80000000u;
 
 struct MsgRegs {  // the 88-byte icrc_write_msg in scalar registers (uniform)
-    uint32_t s[22];
+    uint32_t s[kMsgDwords];
     int idx;  // message index held, -1 = none
 };
 
@@ -952,13 +768,8 @@ __device__ __forceinline__ uint32_t msg_u32(const MsgRegs &m, int dw) { return m
 __device__ __forceinline__ uint64_t msg_u64(const MsgRegs &m, int dw) {
     return static_cast<uint64_t>(msg_u32(m, dw)) | (static_cast<uint64_t>(msg_u32(m, dw + 1)) << 32);
 }
-// icrc_write_msg dword offsets
-enum : int {
-    kMLocalVa = 0, kMRemoteVa = 2, kMPayloadOff = 4, kMOutOff = 6, kMTotal = 8, kMRethLen = 9, kMPmtu = 10,
-    kMRkey = 11, kMDqpn = 12, kMPsn = 13, kMSrcIp = 14, kMDstIp = 15, kMFirst = 16, kMNpk = 17, kMSlot = 18,
-    kMMsnId = 19, kMKind = 20, kMsgDwords = 22
-};
-static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout");
+__device__ __forceinline__ uint32_t msg_kind(const MsgRegs &m) { return msg_u32(m, kMKind) & 0xffu; }
+__device__ __forceinline__ uint32_t msg_flags(const MsgRegs &m) { return (msg_u32(m, kMKind) >> 16) & 0xffu; }
 
 // Message descriptors are read with scalar loads (uniform index, constant address space): they
 // count in lgkmcnt, so fetching one inside the row ring leaves the ring's vmcnt accounting exact
@@ -966,12 +777,10 @@ static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout")
 using ConstU32 = const __attribute__((address_space(4))) uint32_t;
 
 __device__ __forceinline__ uint32_t msg_first_packet(const icrc_write_msg *msgs, int idx) {
-    return ((ConstU32 *)reinterpret_cast<uintptr_t>(msgs + idx))[16];  // icrc_write_msg::first_packet
+    return ((ConstU32 *)reinterpret_cast<uintptr_t>(msgs + idx))[kMFirst];
 }
 
-__device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t nmsgs, int idx, MsgRegs &m,
-                                          uint32_t lane) {
-    (void)lane;
+__device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t nmsgs, int idx, MsgRegs &m) {
     m.idx = idx;
     if (static_cast<uint32_t>(idx) < nmsgs) {
         ConstU32 *w = (ConstU32 *)reinterpret_cast<uintptr_t>(msgs + idx);
@@ -983,92 +792,167 @@ __device__ __forceinline__ void msg_fetch(const icrc_write_msg *msgs, uint32_t n
     }
 }
 
-__device__ __forceinline__ void seg_info(const MsgRegs &m, uint32_t s, SegInfo &g) {
-    const uint32_t total = msg_u32(m, kMTotal), pmtu = msg_u32(m, kMPmtu);
-    const bool by_remote = ((msg_u32(m, kMKind) >> 16) & ICRC_WRITE_SEG_BY_REMOTE_VA) != 0u;
-    const uint32_t lva = by_remote ? msg_u32(m, kMRemoteVa) : msg_u32(m, kMLocalVa);  // low 32 bits (constant index: m stays in registers)
-    uint32_t first = pmtu - lva % pmtu;
-    first = total < first ? total : first;
-    if (s == 0) {
-        g.start = 0;
-        g.len = first;
-    } else {
-        g.start = first + (s - 1) * pmtu;
-        const uint32_t rem = total - g.start;
-        g.len = rem < pmtu ? rem : pmtu;
-    }
-    g.pad = (4u - (g.len & 3u)) & 3u;
-    g.L = 56u + g.len + g.pad + 4u;
-    g.out = msg_u64(m, kMOutOff) + static_cast<uint64_t>(s) * msg_u32(m, kMSlot);
-    g.src = msg_u64(m, kMPayloadOff) + g.start;
-    const int N = 1 + static_cast<int>((g.L - 4u) >> 2);
-    g.R = (N + 63) >> 6;
-    g.k0 = N - 64 * g.R;
+// One packet of a message (wave-uniform): segment s (generate_segments_from_request,
+// common.rs:152-176, or one READ REQUEST packet, read.rs:33-89) and where its bytes go.
+struct SendPlan {
+    uint64_t src;   // payload offset in d_src
+    uint64_t out;   // packet offset in d_wire
+    uint32_t start; // payload byte offset of the segment within the message
+    uint32_t plen;  // payload bytes
+    uint32_t hw;    // header words: 14 (IPv4 + UDP + BTH + RETH) or 18 (+ secondary RETH)
+    uint32_t L;     // wire length: 4 hw + plen + pad + 4
+    int k0;         // stream word index of lane 0 in ring row 0 (rows aligned to kRows)
+    uint32_t pk;    // packet index (0xFFFFFFFF: empty slot)
+    bool fits;      // a message, a pmtu, payload inside d_src, slot inside d_wire, L <= 0xFFFF
+    bool fast;      // fits, both ends 4-byte aligned, at most kRows rows
+};
+
+__device__ __forceinline__ void plan_empty(SendPlan &g) {
+    g.src = g.out = 0;
+    g.start = g.plen = g.L = 0;
+    g.hw = 14;
+    g.k0 = 0;
+    g.pk = 0xFFFFFFFFu;
+    g.fits = g.fast = false;
 }
 
+__device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const uint8_t *src, uint64_t src_bytes,
+                                            const uint8_t *wire, uint64_t wire_bytes, SendPlan &g) {
+    plan_empty(g);
+    g.pk = pk;
+    const uint32_t s = pk - msg_u32(m, kMFirst);
+    const uint32_t kind = msg_kind(m), pmtu = msg_u32(m, kMPmtu), total = msg_u32(m, kMTotal);
+    if (kind == 2u) {  // READ REQUEST: one packet, no payload, a second RETH (read.rs:57-74)
+        g.hw = 18;
+    } else {
+        if (kind > 2u || pmtu == 0u) return;
+        const bool by_remote = (msg_flags(m) & ICRC_WRITE_SEG_BY_REMOTE_VA) != 0u;
+        const uint32_t lva = by_remote ? msg_u32(m, kMRemoteVa) : msg_u32(m, kMLocalVa);  // low 32 bits suffice
+        uint32_t first = pmtu - lva % pmtu;
+        first = total < first ? total : first;
+        if (s == 0) {
+            g.plen = first;
+        } else {
+            g.start = first + (s - 1) * pmtu;
+            const uint32_t rem = total - g.start;
+            g.plen = rem < pmtu ? rem : pmtu;
+        }
+    }
+    const uint32_t pad = (4u - (g.plen & 3u)) & 3u;
+    g.L = 4u * g.hw + g.plen + pad + 4u;
+    g.out = msg_u64(m, kMOutOff) + static_cast<uint64_t>(s) * msg_u32(m, kMSlot);
+    g.src = msg_u64(m, kMPayloadOff) + g.start;
+    g.fits = g.plen <= src_bytes && g.src <= src_bytes - g.plen && g.L <= wire_bytes && g.out <= wire_bytes - g.L &&
+             g.L <= 0xFFFFu;  // IPv4 total length (PacketWriter::write: LengthTooLong, packet_processor.rs:226)
+    const int N = 1 + static_cast<int>((g.L - 4u) >> 2);
+    g.k0 = N - 64 * kRows;
+    g.fast = g.fits && g.L <= 4u * (64u * kRows - 1u) + 4u &&
+             ((reinterpret_cast<uintptr_t>(src) + g.src) & 3u) == 0 &&
+             ((reinterpret_cast<uintptr_t>(wire) + g.out) & 3u) == 0;
+}
 
-// IPv4 (write_ip_udp_header, packet_processor.rs:307-332) + UDP + BTH (set_from_common_meta,
-// packet.rs:145-153 on a zeroed buffer) + RETH (197-201).
-__device__ __forceinline__ void build_header(const MsgRegs &m, uint32_t s, const SegInfo &g, PacketHdr &h) {
-    const uint32_t n = msg_u32(m, kMNpk);
-    const uint32_t kind = msg_u32(m, kMKind) & 0xffu, tran = (msg_u32(m, kMKind) >> 8) & 0xffu;
+// Header words (LE u32 of header bytes 4w .. 4w+3): IPv4 (write_ip_udp_header,
+// packet_processor.rs:307-332) + UDP + BTH (set_from_common_meta, packet.rs:145-153, on a zeroed
+// buffer) + RETH (197-201) [+ secondary RETH, read requests].  Returned as lane w of one VGPR.
+__device__ __forceinline__ uint32_t header_lanes(const MsgRegs &m, const SendPlan &g, uint32_t lane) {
+    const uint32_t s = g.pk - msg_u32(m, kMFirst);
+    const uint32_t n = msg_u32(m, kMNpk), kind = msg_kind(m), tran = (msg_u32(m, kMKind) >> 8) & 0xffu;
+    const uint32_t flags = msg_flags(m);
     const bool only = n == 1u, last = s + 1u == n;
-    uint32_t op;
-    if (kind == 0u) op = only ? 0x0Au : (s == 0u ? 0x06u : (last ? 0x08u : 0x07u));
-    else op = only ? 0x10u : (s == 0u ? 0x0Du : (last ? 0x0Fu : 0x0Eu));
-    const uint32_t ack = (only || last) ? 1u : 0u;
+    uint32_t op, ack;
+    if (kind == 0u) {  // Write::handle (write.rs:31-96)
+        op = only ? 0x0Au : (s == 0u ? 0x06u : (last ? 0x08u : 0x07u));
+        ack = (only || last) ? 1u : 0u;
+    } else if (kind == 1u) {  // ReadResponse::handle (read_response.rs:30-95)
+        op = only ? 0x10u : (s == 0u ? 0x0Du : (last ? 0x0Fu : 0x0Eu));
+        ack = (only || last) ? 1u : 0u;
+    } else {  // Read::handle: ack_req = the request is signaled (read.rs:37)
+        op = 0x0Cu;
+        ack = (flags & ICRC_WRITE_ACK_REQ) ? 1u : 0u;
+    }
+    const uint32_t sol = (flags & ICRC_WRITE_SOLICITED) ? 0x80u : 0u;
+    const uint32_t pad = (4u - (g.plen & 3u)) & 3u;
     const uint32_t msn_id = msg_u32(m, kMMsnId), msn = msn_id & 0xffffu, ipid = msn_id >> 16;
     const uint32_t psn = (msg_u32(m, kMPsn) + s) & 0xffffffu;
     const uint64_t va = msg_u64(m, kMRemoteVa) + g.start;
-    h.w[0] = 0x45u | (((g.L >> 8) & 0xffu) << 16) | ((g.L & 0xffu) << 24);
-    h.w[1] = bswap16(ipid);
-    h.w[2] = 0x1140u;  // TTL 64, protocol UDP, checksum 0
-    h.w[3] = bswap32(msg_u32(m, kMSrcIp));
-    h.w[4] = bswap32(msg_u32(m, kMDstIp));
-    h.w[5] = bswap16(4791u) | (bswap16(4791u) << 16);
-    h.w[6] = bswap16(g.L - 20u);
-    h.w[7] = (((tran << 5) & 0xffu) | op) | ((g.pad << 5) << 8) | (bswap16(msn) << 16);
-    h.w[8] = bswap32(msg_u32(m, kMDqpn) & 0xffffffu);
-    h.w[9] = bswap32(psn) | (ack << 7);
-    h.w[10] = bswap32(static_cast<uint32_t>(va >> 32));
-    h.w[11] = bswap32(static_cast<uint32_t>(va));
-    h.w[12] = bswap32(msg_u32(m, kMRkey));
-    h.w[13] = bswap32(msg_u32(m, kMRethLen));
-    if ((msg_u32(m, kMKind) >> 16) & ICRC_WRITE_FILL_IPV4_CSUM) {
+    uint32_t w[18];
+    w[0] = 0x45u | (((g.L >> 8) & 0xffu) << 16) | ((g.L & 0xffu) << 24);
+    w[1] = bswap16(ipid);
+    w[2] = 0x1140u;  // TTL 64, protocol UDP, checksum 0
+    w[3] = bswap32(msg_u32(m, kMSrcIp));
+    w[4] = bswap32(msg_u32(m, kMDstIp));
+    w[5] = bswap16(4791u) | (bswap16(4791u) << 16);
+    w[6] = bswap16(g.L - 20u);
+    w[7] = (((tran << 5) & 0xffu) | op) | ((sol | (pad << 5)) << 8) | (bswap16(msn) << 16);
+    w[8] = bswap32(msg_u32(m, kMDqpn) & 0xffffffu);
+    w[9] = bswap32(psn) | (ack << 7);
+    w[10] = bswap32(static_cast<uint32_t>(va >> 32));
+    w[11] = bswap32(static_cast<uint32_t>(va));
+    w[12] = bswap32(msg_u32(m, kMRkey));
+    w[13] = bswap32(msg_u32(m, kMRethLen));
+    // secondary RETH of a read request: the local SGE (va, lkey, len)
+    w[14] = bswap32(msg_u32(m, kMLocalVa + 1));
+    w[15] = bswap32(msg_u32(m, kMLocalVa));
+    w[16] = bswap32(msg_u32(m, kMLkey));
+    w[17] = bswap32(msg_u32(m, kMTotal));
+    if (flags & ICRC_WRITE_FILL_IPV4_CSUM) {
         // RFC 791 one's-complement sum of the ten big-endian 16-bit header words
         const uint32_t src = msg_u32(m, kMSrcIp), dst = msg_u32(m, kMDstIp);
         uint32_t sum = 0x4500u + (g.L & 0xFFFFu) + ipid + 0x4011u + (src >> 16) + (src & 0xFFFFu) + (dst >> 16) +
                        (dst & 0xFFFFu);
         sum = (sum & 0xFFFFu) + (sum >> 16);
         sum = (sum & 0xFFFFu) + (sum >> 16);
-        h.w[2] |= bswap16(~sum & 0xFFFFu) << 16;
+        w[2] |= bswap16(~sum & 0xFFFFu) << 16;
     }
-}
-
-__device__ __forceinline__ uint32_t header_word(const PacketHdr &h, int pw) {
     uint32_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 14; ++i) v = (pw == i) ? h.w[i] : v;
+    for (int i = 0; i < 18; ++i) v = (lane == static_cast<uint32_t>(i) && static_cast<uint32_t>(i) < g.hw) ? w[i] : v;
     return v;
 }
 
 // Word pw of the packet for the byte-wise path: header, payload bytes from d_src, zero pad.
-__device__ __forceinline__ uint32_t packet_word_bytes(const PacketHdr &h, const uint8_t *src, uint64_t src_bytes,
-                                                      const SegInfo &g, int pw) {
+__device__ __forceinline__ uint32_t packet_word_bytes(uint32_t hvec, const uint8_t *src, uint64_t src_bytes,
+                                                      const SendPlan &g, int pw) {
+    const uint32_t h = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((pw & 63) << 2, static_cast<int>(hvec)));
     if (pw < 0) return 0u;
-    if (pw < 14) return header_word(h, pw);
+    if (pw < static_cast<int>(g.hw)) return h;
     uint32_t w = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const uint32_t q = 4u * static_cast<uint32_t>(pw) + t - 56u;
+        const uint32_t q = 4u * static_cast<uint32_t>(pw) + t - 4u * g.hw;
         const uint64_t a = g.src + q;
-        const uint32_t b = (q < g.len && a < src_bytes) ? src[a] : 0u;
+        const uint32_t b = (q < g.plen && a < src_bytes) ? src[a] : 0u;
         w |= b << (8 * t);
     }
     return w;
 }
 
-template <int RD>
+// Per-wave result buffers (pkt_len, icrc) keyed by 64-packet block; the flush is a buffer store
+// every record issues (out of range when there is nothing to flush): no branch around a store.
+struct SendResults {
+    ResultBuf len, crc;
+    int block;
+};
+
+__device__ __forceinline__ void send_record(SendResults &r, uint32_t *pkt_len, uint32_t *icrc_out, uint32_t npk,
+                                            uint32_t pk, uint32_t L, uint32_t crc, bool valid, uint32_t lane) {
+    const int blk = static_cast<int>(pk >> 6);
+    const bool flush = valid && blk != r.block && r.len.valid != 0;
+    const uint32_t idx = static_cast<uint32_t>(r.block) * 64u + lane;
+    const bool mine = flush && ((r.len.valid >> lane) & 1ull);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(pkt_len, 0, pkt_len ? static_cast<int>(npk * 4u) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(icrc_out, 0, icrc_out ? static_cast<int>(npk * 4u) : 0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(r.len.v, rl, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(r.crc.v, rc, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
+    if (flush) r.len.valid = r.crc.valid = 0;
+    if (valid) {
+        r.block = blk;
+        rb_put(r.len, pk, L);
+        rb_put(r.crc, pk, crc);
+    }
+}
+
+template <int D>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const uint8_t *src, uint64_t src_bytes,
                                                                           const icrc_write_msg *msgs, uint32_t nmsgs,
                                                                           uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
@@ -1103,201 +987,217 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     }
     mlo = __builtin_amdgcn_readfirstlane(mlo);
 
-    // cursors: packet index, its message (one dword per lane), segment, row
-    struct Cur {
-        uint32_t pk;
-        MsgRegs m;
-        SegInfo g;
-        int j;
-        bool fast, fits;
-    };
-    Cur lc, pc;
-    // cur.fits: the packet has a message, a non-zero pmtu, its payload inside d_src and its slot
-    // inside d_wire; cur.fast: it fits and both payload and slot are 4-byte aligned.
-    auto locate = [&](Cur &cur, uint32_t pk) __attribute__((always_inline)) {
-        cur.pk = pk;
-        cur.j = 0;
-        cur.fast = cur.fits = false;
-        cur.g.R = 0;
-        cur.g.L = 0;
-        cur.g.k0 = 0;
-        cur.g.src = 0;
-        cur.g.out = 0;
-        cur.g.len = 0;
-        if (pk >= hi) return;
-        while (cur.m.idx < static_cast<int>(nmsgs) &&
-               (cur.m.idx < 0 || pk >= msg_u32(cur.m, kMFirst) + msg_u32(cur.m, kMNpk))) {
-            const int next = cur.m.idx < 0 ? mlo : cur.m.idx + 1;
-            msg_fetch(msgs, nmsgs, next, cur.m, lane);
-        }
-        if (cur.m.idx >= static_cast<int>(nmsgs) || pk < msg_u32(cur.m, kMFirst) || msg_u32(cur.m, kMPmtu) == 0u)
-            return;
-        SegInfo g;
-        seg_info(cur.m, pk - msg_u32(cur.m, kMFirst), g);
-        cur.fits = g.len <= src_bytes && g.src <= src_bytes - g.len && g.L <= wire_bytes &&
-                   g.out <= wire_bytes - g.L && g.len <= 0x10000u;
-        if (!cur.fits) return;
-        cur.fast = ((reinterpret_cast<uintptr_t>(src) + g.src) & 3u) == 0 &&
-                   ((reinterpret_cast<uintptr_t>(wire) + g.out) & 3u) == 0;
-        cur.g = g;
-    };
-    auto advance = [&](Cur &cur) __attribute__((always_inline)) {  // next packet taking the fast path
-        uint32_t pk = cur.pk + 1u;
-        for (;;) {
-            locate(cur, pk);
-            if (pk >= hi || cur.fast) return;
-            ++pk;
-        }
-    };
-    lc.m.idx = pc.m.idx = -1;
+    // load side: one message cursor; the plan of packet pk (or an empty slot past hi)
+    MsgRegs lm;
+    lm.idx = -1;
+    uint32_t next_pk = lo;
     bool slow_seen = false;
-    locate(lc, lo);
-    if (!lc.fast) advance(lc);
-    locate(pc, lo);
-    if (!pc.fast) {
-        slow_seen = pc.pk < hi;
-        advance(pc);
-    }
-
-    ResultBuf rb_len, rb_crc;
-    rb_len.v = rb_crc.v = 0;
-    rb_len.valid = rb_crc.valid = 0;
-    int rb_block = -1;
-    auto record = [&](uint32_t pk, uint32_t L, uint32_t crc) __attribute__((always_inline)) {
-        const int blk = static_cast<int>(pk >> 6);
-        if (blk != rb_block) {
-            if (rb_len.valid) {
-                const uint32_t base = static_cast<uint32_t>(rb_block) * 64u + lane;
-                if ((rb_len.valid >> lane) & 1ull) {
-                    if (pkt_len) pkt_len[base] = rb_len.v;
-                    if (icrc_out) icrc_out[base] = rb_crc.v;
-                }
-                rb_len.valid = rb_crc.valid = 0;
-            }
-            rb_block = blk;
+    auto locate = [&](MsgRegs &m, uint32_t pk, SendPlan &g) __attribute__((always_inline)) {
+        while (m.idx < static_cast<int>(nmsgs) && (m.idx < 0 || pk >= msg_u32(m, kMFirst) + msg_u32(m, kMNpk)))
+            msg_fetch(msgs, nmsgs, m.idx < 0 ? mlo : m.idx + 1, m);
+        if (m.idx >= static_cast<int>(nmsgs) || pk < msg_u32(m, kMFirst)) {
+            plan_empty(g);
+            g.pk = pk;  // no message: not fits
+            return;
         }
-        rb_put(rb_len, pk, L);
-        rb_put(rb_crc, pk, crc);
+        plan_packet(m, pk, src, src_bytes, wire, wire_bytes, g);
     };
-
-    auto load_row = [&](uint32_t &dst) __attribute__((always_inline)) {
-        const int nrec = lc.g.R > 0 ? static_cast<int>((lc.g.len + 3u) & ~3u) : 0;
+    // next packet of the ring (fast packets only), its header lanes and its row loads
+    auto fill = [&](SendPlan &g, uint32_t &hvec, uint32_t (&u)[kRows]) __attribute__((always_inline)) {
+        plan_empty(g);
+        while (next_pk < hi) {
+            locate(lm, next_pk, g);
+            ++next_pk;
+            if (g.fast) break;
+            slow_seen = true;
+            plan_empty(g);
+        }
+        hvec = g.fast ? header_lanes(lm, g, lane) : 0u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(src) + (lc.g.R > 0 ? lc.g.src : 0), 0, nrec, 0x00020000);
-        // payload byte offset of this lane's word: 4 * pw - 56 (negative -> out of range -> 0)
-        const uint32_t voff = 4u * static_cast<uint32_t>(lc.g.k0 - 1 + static_cast<int>(lane) + 64 * lc.j) - 56u;
-        dst = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(voff), 0, 0);  // default policy: copies run ~6 % faster than nt (r01_membench_copy.json)
-        if (lc.g.R > 0) {
-            lc.j += 1;
-            if (lc.j == lc.g.R) advance(lc);
-        }
+            const_cast<uint8_t *>(src) + (g.fast ? g.src : 0), 0, g.fast ? static_cast<int>((g.plen + 3u) & ~3u) : 0,
+            0x00020000);
+        // payload byte offset of this lane's word: 4 pw - 4 hw (before the payload: out of range -> 0)
+        const uint32_t vb = 4u * static_cast<uint32_t>(g.k0 - 1 + static_cast<int>(lane)) - 4u * g.hw;
+#pragma unroll
+        for (int j = 0; j < kRows; ++j)
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vb + 256u * j), 0, 0);
     };
 
-    constexpr int kRD = RD;
-    uint32_t ring[kRD];
-    static_for<kRD>([&](auto ic) __attribute__((always_inline)) -> bool {
-        load_row(ring[decltype(ic)::value]);
-        return true;
-    });
-    PacketHdr h;
-    uint32_t hvec = 0;  // header word w in lane w (w < 14), one ds_bpermute per header row
-    auto spread_header = [&]() __attribute__((always_inline)) {
+    SendResults res;
+    res.len.v = res.crc.v = 0;
+    res.len.valid = res.crc.valid = 0;
+    res.block = -1;
+    // process side: one packet of the ring
+    auto process = [&](const SendPlan &g, uint32_t hvec, uint32_t (&u)[kRows]) __attribute__((always_inline)) {
+        // rows holding stream words 0..9 (head masks) and packet words 0..hw-1 (header)
+        const int j0 = (-g.k0) >> 6;                     // row of stream word 0 (the FF prefix word)
+        const int jh = (1 - g.k0) >> 6;                  // row of packet word 0
+        const int pw0 = g.k0 - 1 + static_cast<int>(lane) + 64 * jh;  // this lane's packet word in row jh
+        const uint32_t hA = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((pw0 & 63) << 2, static_cast<int>(hvec)));
+        const uint32_t hB = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(((pw0 + 64) & 63) << 2, static_cast<int>(hvec)));
+        const bool inA = pw0 >= 0 && pw0 < static_cast<int>(g.hw);
+        const bool inB = pw0 + 64 >= 0 && pw0 + 64 < static_cast<int>(g.hw);
+        const uint32_t mA = head_mask(g.k0 + static_cast<int>(lane) + 64 * j0);
+        const uint32_t mB = head_mask(g.k0 + static_cast<int>(lane) + 64 * (j0 + 1));
+        const uint32_t room = 4u * g.hw + g.plen;  // bytes before the pad
+        const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
+            wire + g.out, 0, g.fast ? static_cast<int>(g.L - 4u) : 0, 0x00020000);
+        uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < 14; ++k) hvec = lane == static_cast<uint32_t>(k) ? h.w[k] : hvec;
-    };
-    if (pc.pk < hi) {
-        build_header(pc.m, pc.pk - msg_u32(pc.m, kMFirst), pc.g, h);
-        spread_header();
-    }
-    uint32_t acc = 0;
-    while (pc.pk < hi) {
-        static_for<kRD>([&](auto ic) __attribute__((always_inline)) -> bool {
-            constexpr int i = decltype(ic)::value;
-            if (pc.pk >= hi) return false;
-            const int pw = pc.g.k0 - 1 + static_cast<int>(lane) + 64 * pc.j;
-            uint32_t w = ring[i];
-            // last payload word (only in the packet's last row): keep only the payload bytes
-            if (pc.j == pc.g.R - 1) {
-                const int room = static_cast<int>(56u + pc.g.len) - 4 * pw;  // payload bytes from this word on
-                if (room < 4) w = room <= 0 ? 0u : (w & ((1u << (8 * room)) - 1u));
+        for (int j = 0; j < kRows; ++j) {
+            const int pw = g.k0 - 1 + static_cast<int>(lane) + 64 * j;
+            uint32_t w = u[j];
+            w = (j == jh && inA) ? hA : ((j == jh + 1 && inB) ? hB : w);
+            if (j == kRows - 1) {  // the packet's last word: payload bytes only, then the zero pad
+                const int keep = static_cast<int>(room) - 4 * pw;
+                w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
-            if (pc.j < 2) {  // header words: lane w of hvec holds header word w
-                const uint32_t hw = static_cast<uint32_t>(
-                    __builtin_amdgcn_ds_bpermute(static_cast<int>(static_cast<uint32_t>(pw) << 2), static_cast<int>(hvec)));
-                w = (pw >= 0 && pw < 14) ? hw : w;
-            }
-            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(wire + pc.g.out, 0,
-                                                                                static_cast<int>(pc.g.L - 4u), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(w, os, static_cast<int>(4u * static_cast<uint32_t>(pw)), 0, 0);
-            uint32_t u = w;
-            if (pc.j < 2) u |= head_mask(pw + 1);
-            if (pc.j == 0) acc = u;
-            else acc = step_m64(lds, acc, u, c);
-            pc.j += 1;
-            if (pc.j == pc.g.R) {
-                const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
-                if (lane == 0) *reinterpret_cast<uint32_t *>(wire + pc.g.out + pc.g.L - 4u) = crc;
-                record(pc.pk, pc.g.L, crc);
-                const uint32_t before = pc.pk;
-                advance(pc);
-                if (pc.pk != before + 1u && before + 1u < hi) slow_seen = true;
-                if (pc.pk < hi) {
-                    build_header(pc.m, pc.pk - msg_u32(pc.m, kMFirst), pc.g, h);
-                    spread_header();
-                }
-            }
-            load_row(ring[i]);
+            const uint32_t uu = w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u));
+            acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
+        }
+        const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
+        const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
+            wire + g.out, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
+        send_record(res, pkt_len, icrc_out, npk, g.pk, g.L, crc, g.fast, lane);
+    };
+
+    constexpr int B = D + 1;
+    SendPlan g[B];
+    uint32_t hv[B];
+    uint32_t u[B][kRows];
+#pragma unroll
+    for (int d = 0; d < D; ++d) fill(g[d], hv[d], u[d]);
+    for (;;) {
+        const bool more = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            if (!g[b].fast) return false;  // the ring ran dry: every later slot is empty too
+            fill(g[bp], hv[bp], u[bp]);
+            process(g[b], hv[b], u[b]);
             return true;
         });
+        if (!more) break;
     }
-    if (rb_len.valid && (rb_len.valid >> lane) & 1ull) {
-        const uint32_t base = static_cast<uint32_t>(rb_block) * 64u + lane;
-        if (pkt_len) pkt_len[base] = rb_len.v;
-        if (icrc_out) icrc_out[base] = rb_crc.v;
+    // last partial block of results
+    {
+        const bool mine = res.len.valid && ((res.len.valid >> lane) & 1ull);
+        const uint32_t idx = static_cast<uint32_t>(res.block) * 64u + lane;
+        if (mine) {
+            if (pkt_len) pkt_len[idx] = res.len.v;
+            if (icrc_out) icrc_out[idx] = res.crc.v;
+        }
     }
 
-    // Byte-wise path for packets whose payload or slot is not 4-byte aligned; packets that do not
-    // fit (no message, payload outside d_src, slot outside d_wire) report length 0.
+    // Byte-wise path for packets whose payload or slot is not 4-byte aligned (or longer than 17
+    // rows); packets that do not fit (no message, payload outside d_src, slot outside d_wire,
+    // L > 0xFFFF) report length 0.
     if (slow_seen) {
-        Cur sc;
-        sc.m.idx = -1;
+        MsgRegs sm;
+        sm.idx = -1;
         for (uint32_t pk = lo; pk < hi; ++pk) {
-            locate(sc, pk);
-            if (sc.fast) continue;
-            if (!sc.fits) {
+            SendPlan sg;
+            locate(sm, pk, sg);
+            if (sg.fast) continue;
+            if (!sg.fits) {
                 if (lane == 0) {
                     if (pkt_len) pkt_len[pk] = 0u;
                     if (icrc_out) icrc_out[pk] = 0u;
                 }
                 continue;
             }
-            PacketHdr hs;
-            build_header(sc.m, pk - msg_u32(sc.m, kMFirst), sc.g, hs);
-            uint8_t *out = wire + sc.g.out;
+            const uint32_t hvec = header_lanes(sm, sg, lane);
+            uint8_t *out = wire + sg.out;
+            const int N = 1 + static_cast<int>((sg.L - 4u) >> 2);
+            const int R = (N + 63) >> 6;
+            const int k0 = N - 64 * R;
             uint32_t a = 0;
-            for (int r = 0; r < sc.g.R; ++r) {
-                const int pw = sc.g.k0 - 1 + static_cast<int>(lane) + 64 * r;
-                const uint32_t w = packet_word_bytes(hs, src, src_bytes, sc.g, pw);
-                if (pw >= 0 && static_cast<uint32_t>(4 * pw) < sc.g.L - 4u) {
+            for (int r = 0; r < R; ++r) {
+                const int pw = k0 - 1 + static_cast<int>(lane) + 64 * r;
+                const uint32_t w = packet_word_bytes(hvec, src, src_bytes, sg, pw);
+                if (pw >= 0 && static_cast<uint32_t>(4 * pw) < sg.L - 4u) {
                     out[4 * pw] = static_cast<uint8_t>(w);
                     out[4 * pw + 1] = static_cast<uint8_t>(w >> 8);
                     out[4 * pw + 2] = static_cast<uint8_t>(w >> 16);
                     out[4 * pw + 3] = static_cast<uint8_t>(w >> 24);
                 }
-                uint32_t u = w;
-                if (r < 2) u |= head_mask(pw + 1);
-                a = (r == 0) ? u : step_m64(lds, a, u, c);
+                uint32_t uu = w;
+                if (r < 2) uu |= head_mask(pw + 1);
+                a = (r == 0) ? uu : step_m64(lds, a, uu, c);
             }
             const uint32_t crc = ~wave_xor(final_mul(lds, a, c.fin));
             if (lane == 0) {
-                uint8_t *t = out + sc.g.L - 4u;
+                uint8_t *t = out + sg.L - 4u;
                 t[0] = static_cast<uint8_t>(crc);
                 t[1] = static_cast<uint8_t>(crc >> 8);
                 t[2] = static_cast<uint8_t>(crc >> 16);
                 t[3] = static_cast<uint8_t>(crc >> 24);
-                if (pkt_len) pkt_len[pk] = sc.g.L;
+                if (pkt_len) pkt_len[pk] = sg.L;
                 if (icrc_out) icrc_out[pk] = crc;
             }
+        }
+    }
+}
+
+// ---- receive-side auto-ACK (generate_ack, net/util.rs:134-170) -------------------------------------
+// One thread per received packet.  The ACK is needed exactly when every receive handler would send
+// one (write_first.rs:35-82 and the ten other handlers): the packet parsed (status OK), its ICRC
+// verified, it is not itself an ACK, ack_req is set, the QP exists and is not in the error state,
+// and psn == the QP's expected PSN.  The 48-byte packet is generate_ack's PacketWriter output:
+// 192.168.0.3 -> 192.168.0.2, ip_id 1, ports 4791, BTH {Acknowledge, RC, pkey = the packet's
+// pkey, dqpn = peer_qpn, psn = expected_psn}, AETH {Ack, 0x1f, msn = pkey}, ICRC.  The ICRC of
+// these 44 bytes (+ the FF x 8 prefix, masked header) is computed byte-serially in the thread from
+// a 1 KiB byte table in LDS: 52 lookups per ACK, ACKs are one per message, not per byte.
+__global__ __launch_bounds__(256) void icrc_ack_kernel(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n,
+                                                       uint8_t *out, uint32_t stride, uint32_t *out_len, uint32_t mode) {
+    __shared__ uint32_t T[256];
+    {
+        uint32_t c = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : (c >> 1);
+        T[threadIdx.x] = c;
+    }
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(desc + i);
+        const uint32_t psn = dw[13], w15 = dw[15], w16 = dw[16], w17 = dw[17];
+        const uint32_t pkey = w15 & 0xFFFFu, flags = w16 & 0xFFu;
+        const uint32_t icrc_ok = w17 & 0xFFu, status = (w17 >> 8) & 0xFFu;
+        const icrc_ack_ctx x = ctx[i];
+        const bool need = status == ICRC_RX_OK && icrc_ok == ICRC_VERIFY_OK && !(flags & ICRC_RX_ACKNOWLEDGE) &&
+                          (flags & ICRC_RX_ACK_REQ) && (x.flags & ICRC_ACK_CTX_QP_VALID) && psn == x.expected_psn;
+        if (out_len) out_len[i] = need ? ((mode & ICRC_ACK_UDP_PAYLOAD_ONLY) ? 20u : 48u) : 0u;
+        if (!need) continue;
+        uint32_t w[12];
+        w[0] = 0x30000045u;  // 0x45, DSCP 0, total length 48
+        w[1] = 0x00000100u;  // ip_id 1, flags / fragment 0
+        w[2] = 0x00001140u;  // TTL 64, UDP, checksum 0
+        w[3] = 0x0300A8C0u;  // 192.168.0.3 (util.rs:158)
+        w[4] = 0x0200A8C0u;  // 192.168.0.2
+        w[5] = 0xB712B712u;  // 4791 -> 4791
+        w[6] = 0x00001C00u;  // UDP length 28, checksum 0
+        w[7] = 0x11u | (bswap16(pkey) << 16);             // Acknowledge, RC, pkey
+        w[8] = bswap32(x.peer_qpn & 0xFFFFFFu);           // dqpn = peer_qpn
+        w[9] = bswap32(x.expected_psn & 0xFFFFFFu);       // ack_req 0, psn = expected_psn
+        w[10] = bswap32(pkey) | 0x1Fu;                    // AETH: Ack, value 0x1f, msn = pkey
+        uint32_t c = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c = T[(c ^ 0xFFu) & 0xFFu] ^ (c >> 8);
+#pragma unroll
+        for (int k = 0; k < 44; ++k) {
+            uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            if (k == 1 || k == 8 || k == 10 || k == 11 || k == 26 || k == 27 || k == 32) b = 0xFFu;
+            c = T[(c ^ b) & 0xFFu] ^ (c >> 8);
+        }
+        w[11] = ~c;
+        uint32_t *o = reinterpret_cast<uint32_t *>(out + static_cast<uint64_t>(i) * stride);
+        if (mode & ICRC_ACK_UDP_PAYLOAD_ONLY) {  // generate_ack's return value: the UDP payload
+#pragma unroll
+            for (int k = 0; k < 5; ++k) o[k] = w[7 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) o[k] = w[k];
         }
     }
 }
@@ -1377,69 +1277,56 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 
 }  // namespace
 
-#define ICRC_LAUNCH(S, D, A) \
-    hipLaunchKernelGGL((icrc_batch_kernel<MODE, S, D, A>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
-#define ICRC_QUAD(V) (void)launch_quad(MODE, V, p, grid, s)
+#define ICRC_LAUNCH(S, D, A, T) \
+    hipLaunchKernelGGL((icrc_batch_kernel<MODE, S, D, A, T>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_LAUNCH_T(S, D, A)          \
+    do {                                \
+        if (p.trailer) ICRC_LAUNCH(S, D, A, true); \
+        else ICRC_LAUNCH(S, D, A, false);          \
+    } while (0)
 
+// Variants: 0 one packet per wave, no pipelining; 13 one chain per wave (S = 1, D = 1); 16 two
+// chains (S = 2, D = 1, the default for long packets); 15 / 18 diagnostics of the S = 1, D = 2
+// shape (loads only / CRC only: wrong results by design); 20, 24-26, 31, 32, 35: the quad / oct
+// kernels (icrc_quad.hip).
 template <int MODE>
 static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     switch (p.variant) {
-    case 0: ICRC_LAUNCH(0, 1, 0); break;
-    case 1: ICRC_LAUNCH(1, 1, 0); break;
-    case 2: ICRC_LAUNCH(2, 1, 0); break;
-    case 3: ICRC_LAUNCH(1, 2, 0); break;
-    case 4: ICRC_LAUNCH(1, 3, 0); break;
-    case 5: ICRC_LAUNCH(2, 2, 0); break;
-    case 6: ICRC_LAUNCH(1, 2, 1); break;  // diagnostic: loads only
-    case 7: ICRC_LAUNCH(1, 2, 2); break;  // diagnostic: CRC only
-    case 8: ICRC_LAUNCH(2, 1, 2); break;  // diagnostic: CRC only, 2 chains
-    case 9: ICRC_LAUNCH(2, 1, 1); break;  // diagnostic: loads only, 2 chains
-    case 10: ICRC_LAUNCH(-16, 0, 0); break;  // row stream, 16 rows in flight per wave
-    case 11: ICRC_LAUNCH(-24, 0, 0); break;  // row stream, 24 rows
-    case 12: ICRC_LAUNCH(-32, 0, 0); break;  // row stream, 32 rows
-    case 13: ICRC_LAUNCH(1, 1, 2 << 2); break;      // variant 1, nt row loads
-    case 14: ICRC_LAUNCH(1, 2, 2 << 2); break;      // variant 3, nt row loads
-    case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2)); break;  // diagnostic: loads only, nt
-    case 16: ICRC_LAUNCH(2, 1, 2 << 2); break;      // variant 2, nt row loads
-    case 17: ICRC_LAUNCH(1, 3, 2 << 2); break;      // variant 4, nt row loads
-    case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2)); break;  // diagnostic: CRC only (same code shape as 15)
-    case 19:  // four packets per wave (icrc_quad.hip): K rows per chunk, D chunks in flight
+    case 0: ICRC_LAUNCH_T(0, 1, 0); break;
+    case 13: ICRC_LAUNCH_T(1, 1, 2 << 2); break;              // S = 1, nt row loads
+    case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2), false); break;  // diagnostic: loads only, nt
+    case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2), false); break;  // diagnostic: CRC only (same shape as 15)
     case 20:
-    case 21:
-    case 22:  // diagnostic: quad kernel, loads only
-    case 23:  // diagnostic: quad kernel, no loads
-    case 24:  // eight packets per wave (W = 8)
+    case 24:
     case 25:
     case 26:
-    case 27:
-    case 28:
-    case 29:
-    case 30:
     case 31:
     case 32:
-    case 33:
-    case 34:
-    case 35:
-    case 36:
-    case 37:
-    case 38: ICRC_QUAD(p.variant); break;
-    default: ICRC_LAUNCH(1, 2, 0); break;
+    case 35: (void)launch_quad(MODE, p.variant, p, grid, s); break;
+    default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }
 }
+#undef ICRC_LAUNCH_T
 #undef ICRC_LAUNCH
-#undef ICRC_QUAD
 
 int launch_long(int mode, const BatchParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool compact = p.long_variant == 1;
-    if (mode == kCompute) {
-        if (compact) hipLaunchKernelGGL((icrc_long_kernel<kCompute, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-        else hipLaunchKernelGGL((icrc_long_kernel<kCompute, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-    } else {
-        if (compact) hipLaunchKernelGGL((icrc_long_kernel<kVerify, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-        else hipLaunchKernelGGL((icrc_long_kernel<kVerify, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-    }
+#define ICRC_LONG(M, C, T) hipLaunchKernelGGL((icrc_long_kernel<M, C, T>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_LONG_M(M)                                  \
+    do {                                                \
+        if (p.long_variant == 1) {                      \
+            if (p.trailer) ICRC_LONG(M, true, true);    \
+            else ICRC_LONG(M, true, false);             \
+        } else {                                        \
+            if (p.trailer) ICRC_LONG(M, false, true);   \
+            else ICRC_LONG(M, false, false);            \
+        }                                               \
+    } while (0)
+    if (mode == kCompute) ICRC_LONG_M(kCompute);
+    else ICRC_LONG_M(kVerify);
+#undef ICRC_LONG_M
+#undef ICRC_LONG
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
@@ -1464,11 +1351,9 @@ int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    switch (p.variant) {  // A/B: 1 (S = 2, D = 1), 2 (S = 1, D = 2), 3 diagnostic (raw header words)
-    case 2: hipLaunchKernelGGL((icrc_rx_kernel<1, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-    case 3: hipLaunchKernelGGL((icrc_rx_kernel<2, 1, 3>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-    default: hipLaunchKernelGGL((icrc_rx_kernel<2, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-    }
+    // A/B only (variant 301): the fused single-pass receive, S = 2, D = 1
+    if (p.trailer) hipLaunchKernelGGL((icrc_rx_kernel<2, 1, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    else hipLaunchKernelGGL((icrc_rx_kernel<2, 1, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
@@ -1489,10 +1374,21 @@ int launch_ipv4_checksum(uint8_t *base, const uint64_t *off, uint64_t stride, ui
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
+int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, uint8_t *out, uint32_t stride,
+               uint32_t *out_len, uint32_t mode, int num_cu, void *stream) {
+    if (n == 0) return ICRC_OK;
+    const uint64_t want = (static_cast<uint64_t>(n) + 255u) / 256u;
+    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 8u;
+    const int grid = static_cast<int>(want < cap ? want : cap);
+    hipLaunchKernelGGL(icrc_ack_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), desc, ctx, n, out,
+                       stride, out_len, mode);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
 int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
     if (p.npackets == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((icrc_packetize_kernel<16>), dim3(grid), dim3(kThreadsPerGroup), 0,
+    hipLaunchKernelGGL((icrc_packetize_kernel<1>), dim3(grid), dim3(kThreadsPerGroup), 0,
                        static_cast<hipStream_t>(stream), p.src, p.src_bytes, p.msgs, p.nmsgs, p.npackets, p.wire,
                        p.wire_bytes, p.pkt_len, p.icrc, p.table);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;

@@ -531,20 +531,15 @@ __global__ __launch_bounds__(NT) void icrc_quad_kernel(BatchParams p) {
 
 }  // namespace
 
-// Quad (W = 16): variant 19: K = 5 rows per chunk, D = 5 chunks in flight; 20: K = 6, D = 4;
-// 21: K = 4, D = 6; 22 / 23: ablations of 20 (loads only / no loads, compute, ragged).
-// Oct (W = 8): 24: K = 10, D = 3; 25: K = 8, D = 4; 26: K = 5, D = 6; 27: K = 12, D = 3;
-// 28: K = 10, D = 4; 29: K = 17, D = 2; 30: K = 7, D = 5; 31 / 32: ablations of 24 (as 22 / 23).
-// 33 / 34: 24 at 8 waves per CU (occupancy probe; 34 without loads); 35: 24 without loads or
-// row steps (strided); 36 / 37 / 38: 35 without final products and routing / header masks / final
-// products.
+// Quad (W = 16): variant 20: K = 6 rows per chunk, D = 4 chunks in flight.  Oct (W = 8): 24 (the
+// default for short packets): K = 10, D = 3; 25: K = 8, D = 4; 26: K = 5, D = 6.  Diagnostics of 24
+// (wrong results by design): 31 loads only (ragged), 32 no loads (ragged), 35 no loads and no row
+// steps (strided: what is left is per-set control).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool ragged = p.off != nullptr || p.len != nullptr;
 #define ICRC_L(W, M, K, D, R, T, ...) \
     hipLaunchKernelGGL((icrc_quad_kernel<W, M, K, D, R, T, ##__VA_ARGS__>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
-#define ICRC_L512(W, M, K, D, R, T, A) \
-    hipLaunchKernelGGL((icrc_quad_kernel<W, M, K, D, R, T, A, 512>), dim3(grid), dim3(512), 0, s, p)
 #define ICRC_Q(W, M, K, D)                                      \
     do {                                                        \
         if (ragged) {                                           \
@@ -558,40 +553,22 @@ int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *str
 #define ICRC_QV(M)                                  \
     do {                                            \
         switch (variant) {                          \
-        case 19: ICRC_Q(16, M, 5, 5); break;        \
-        case 21: ICRC_Q(16, M, 4, 6); break;        \
-        case 24: ICRC_Q(8, M, 10, 3); break;        \
+        case 20: ICRC_Q(16, M, 6, 4); break;        \
         case 25: ICRC_Q(8, M, 8, 4); break;         \
         case 26: ICRC_Q(8, M, 5, 6); break;         \
-        case 27: ICRC_Q(8, M, 12, 3); break;        \
-        case 28: ICRC_Q(8, M, 10, 4); break;        \
-        case 29: ICRC_Q(8, M, 17, 2); break;        \
-        case 30: ICRC_Q(8, M, 7, 5); break;         \
-        default: ICRC_Q(16, M, 6, 4); break;        \
+        default: ICRC_Q(8, M, 10, 3); break;        \
         }                                           \
     } while (0)
-    if (variant == 33 || variant == 34) {  // diagnostic: 8 waves per CU (occupancy probe)
-        if (variant == 33) ICRC_L512(8, kCompute, 10, 3, true, false, 0);
-        else ICRC_L512(8, kCompute, 10, 3, true, false, 2);
-        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
-    }
-    if (variant == 22 || variant == 23 || variant == 31 || variant == 32 || variant == 35 || variant == 36 ||
-        variant == 37 || variant == 38) {
-        if (variant == 22) ICRC_L(16, kCompute, 6, 4, true, false, 1);
-        else if (variant == 23) ICRC_L(16, kCompute, 6, 4, true, false, 2);
-        else if (variant == 31) ICRC_L(8, kCompute, 10, 3, true, false, 1);
+    if (variant == 31 || variant == 32 || variant == 35) {
+        if (variant == 31) ICRC_L(8, kCompute, 10, 3, true, false, 1);
         else if (variant == 32) ICRC_L(8, kCompute, 10, 3, true, false, 2);
-        else if (variant == 35) ICRC_L(8, kCompute, 10, 3, false, false, 3);
-        else if (variant == 36) ICRC_L(8, kCompute, 10, 3, false, false, 4);
-        else if (variant == 38) ICRC_L(8, kCompute, 10, 3, false, false, 6);
-        else ICRC_L(8, kCompute, 10, 3, false, false, 5);
+        else ICRC_L(8, kCompute, 10, 3, false, false, 3);
         return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
     }
     if (mode == kCompute) ICRC_QV(kCompute);
     else ICRC_QV(kVerify);
 #undef ICRC_QV
 #undef ICRC_Q
-#undef ICRC_L512
 #undef ICRC_L
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }

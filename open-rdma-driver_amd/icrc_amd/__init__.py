@@ -94,11 +94,11 @@ WRITE_MSG_DTYPE = np.dtype([
     ("total_len", "<u4"), ("reth_len", "<u4"), ("pmtu", "<u4"), ("rkey", "<u4"), ("dqpn", "<u4"),
     ("psn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("first_packet", "<u4"),
     ("npackets", "<u4"), ("slot_stride", "<u4"), ("msn", "<u2"), ("ip_id", "<u2"),
-    ("kind", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("_pad", "u1", (5,)),
+    ("kind", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("_pad", "u1"), ("lkey", "<u4"),
 ])
-WRITE_FILL_IPV4_CSUM, WRITE_SEG_BY_REMOTE_VA = 0x01, 0x02
+WRITE_FILL_IPV4_CSUM, WRITE_SEG_BY_REMOTE_VA, WRITE_SOLICITED, WRITE_ACK_REQ = 0x01, 0x02, 0x04, 0x08
 assert WRITE_MSG_DTYPE.itemsize == 88
-MSG_WRITE, MSG_READ_RESPONSE = 0, 1
+MSG_WRITE, MSG_READ_RESPONSE, MSG_READ_REQUEST = 0, 1, 2
 
 # icrc_rx_desc (include/icrc.h): one parsed received packet.
 RX_DESC_DTYPE = np.dtype([
@@ -111,6 +111,11 @@ RX_DESC_DTYPE = np.dtype([
 ])
 assert RX_DESC_DTYPE.itemsize == 72
 RX_OK, RX_INVALID_OPCODE, RX_INVALID_TRANS_TYPE, RX_TRUNCATED = 0, 1, 2, 3
+RX_SOLICITED, RX_ACK_REQ, RX_HAS_IMM, RX_HAS_SECONDARY_RETH, RX_ACKNOWLEDGE = 0x01, 0x02, 0x04, 0x08, 0x10
+# icrc_ack_ctx (include/icrc.h): the QP state generate_ack reads (write_first.rs:35-82)
+ACK_CTX_DTYPE = np.dtype([("peer_qpn", "<u4"), ("expected_psn", "<u4"), ("flags", "<u4")])
+ACK_CTX_QP_VALID = 0x1
+ACK_UDP_PAYLOAD_ONLY = 0x1
 EMULATOR_SRC_IP = 0xC0A80002  # 192.168.0.2, hard-coded in send_write_message (common.rs:124)
 
 
@@ -157,6 +162,7 @@ def _load() -> ctypes.CDLL:
         "icrc_write_packetize_device": (i32, [vp, vp, u64, vp, u32, u32, vp, u64, vp, vp, vp]),
         "icrc_rx_parse_device": (i32, [vp, vp, vp, vp, u64, u32, u32, vp, vp, i32, vp, vp]),
         "icrc_ipv4_checksum_device": (i32, [vp, vp, vp, u64, u32, vp, i32, vp]),
+        "icrc_ack_from_rx_device": (i32, [vp, vp, vp, u32, vp, u32, vp, u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -173,12 +179,19 @@ def _check(rc: int, what: str) -> None:
         raise IcrcError(rc, what)
 
 
-def _u8(a) -> np.ndarray:
+def _u8(a, writable: bool = False) -> np.ndarray:
+    """A uint8 view of `a` WITHOUT copying (ndarray, bytearray, memoryview, bytes ...), so that
+    in-place effects (is_icrc_valid's trailer zeroing, trailer writes) reach the caller's buffer.
+    writable=True raises TypeError for read-only buffers instead of silently writing a copy."""
     if isinstance(a, np.ndarray):
         if a.dtype != np.uint8 or not a.flags.c_contiguous:
             raise TypeError("expected a C-contiguous uint8 array")
-        return a
-    return np.frombuffer(bytearray(a), dtype=np.uint8)
+        v = a
+    else:
+        v = np.frombuffer(a, dtype=np.uint8)  # shares memory; read-only for bytes
+    if writable and not v.flags.writeable:
+        raise TypeError("buffer is read-only, but this call writes into it (trailer)")
+    return v
 
 
 def ip4(addr) -> int:
@@ -216,10 +229,11 @@ def compute_icrc(data) -> int:
     return v
 
 
-def is_icrc_valid(buf: np.ndarray, zero_trailer: bool = True) -> bool:
+def is_icrc_valid(buf, zero_trailer: bool = True) -> bool:
     """is_icrc_valid (packet_processor.rs:341-353): zeroes the trailer in place, as the
-    reference does at 350, then recomputes and compares."""
-    a = _u8(buf)
+    reference does at 350, then recomputes and compares.  `buf` may be any writable buffer
+    (ndarray, bytearray, memoryview); a read-only one raises TypeError when zero_trailer."""
+    a = _u8(buf, writable=zero_trailer)
     ok = ctypes.c_int(0)
     _check(lib.icrc_verify(a.ctypes.data, a.size, 1 if zero_trailer else 0, ctypes.byref(ok)),
            "is_icrc_valid")
@@ -229,7 +243,7 @@ def is_icrc_valid(buf: np.ndarray, zero_trailer: bool = True) -> bool:
 def write_ip_udp_header(buf: np.ndarray, src_addr, src_port: int, dest_addr, dest_port: int,
                         total_length: int, ip_identification: int) -> None:
     """write_ip_udp_header (packet_processor.rs:307-332)."""
-    a = _u8(buf)
+    a = _u8(buf, writable=True)
     if a.size < 28:
         raise ValueError("buffer smaller than IPv4+UDP headers")
     lib.icrc_write_ip_udp_header(a.ctypes.data, ip4(src_addr), src_port, ip4(dest_addr), dest_port,
@@ -240,8 +254,8 @@ class PacketWriter:
     """PacketWriter builder (packet_processor.rs:150-265).  write() returns the total length
     or raises IcrcError with the PacketProcessorError code."""
 
-    def __init__(self, buf: np.ndarray):
-        self.buf = _u8(buf)
+    def __init__(self, buf):
+        self.buf = _u8(buf, writable=True)
         self._src = self._sport = self._dst = self._dport = self._ipid = self._msg = None
 
     def src_addr(self, a):
@@ -300,7 +314,7 @@ def compute_icrc_batch(base: np.ndarray, off, lens, write_trailer: bool = False)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     out = np.zeros(off.size, dtype=np.uint32)
-    _check(lib.icrc_compute_batch(_u8(base).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
+    _check(lib.icrc_compute_batch(_u8(base, writable=write_trailer).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
                                   out.ctypes.data, 1 if write_trailer else 0), "icrc_compute_batch")
     return out
 
@@ -309,7 +323,7 @@ def verify_icrc_batch(base: np.ndarray, off, lens, zero_trailer: bool = False) -
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     ok = np.zeros(off.size, dtype=np.uint8)
-    _check(lib.icrc_verify_batch(_u8(base).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
+    _check(lib.icrc_verify_batch(_u8(base, writable=zero_trailer).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
                                  ok.ctypes.data, 1 if zero_trailer else 0), "icrc_verify_batch")
     return ok
 
@@ -377,7 +391,7 @@ class Engine:
         off = np.ascontiguousarray(off, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         out = np.zeros(off.size, dtype=np.uint32)
-        _check(lib.icrc_compute_batch_ex(self.handle, _u8(base).ctypes.data, off.ctypes.data,
+        _check(lib.icrc_compute_batch_ex(self.handle, _u8(base, writable=write_trailer).ctypes.data, off.ctypes.data,
                                          lens.ctypes.data, off.size, out.ctypes.data,
                                          1 if write_trailer else 0), "icrc_compute_batch_ex")
         return out
@@ -395,6 +409,13 @@ class Engine:
         """Batched IPv4 header checksum (icrc_ipv4_checksum_device, responser.rs:321-338)."""
         _check(lib.icrc_ipv4_checksum_device(self.handle, d_base, d_off or None, stride, n, d_csum or None,
                                              1 if fill else 0, stream or None), "icrc_ipv4_checksum_device")
+
+    def ack_from_rx(self, d_desc: int, d_ctx: int, n: int, d_out: int, out_stride: int = 48, d_out_len: int = 0,
+                    udp_payload_only: bool = False, stream: Optional[int] = None) -> None:
+        """Receive-side auto-ACK (icrc_ack_from_rx_device, generate_ack net/util.rs:134-170)."""
+        _check(lib.icrc_ack_from_rx_device(self.handle, d_desc, d_ctx, n, d_out, out_stride, d_out_len or None,
+                                           ACK_UDP_PAYLOAD_ONLY if udp_payload_only else 0, stream or None),
+               "icrc_ack_from_rx_device")
 
     def packetize(self, d_src: int, src_bytes: int, d_msgs: int, nmsgs: int, npackets: int,
                   d_wire: int, wire_bytes: int, d_pkt_len: int = 0, d_icrc: int = 0,
@@ -432,9 +453,12 @@ def write_messages(specs, slot_stride: int = 0, base_out: int = 0) -> np.ndarray
             m["reth_len"] = s["total_len"]
         if "ip_id" not in s:
             m["ip_id"] = 1  # generate_payload_from_msg (net/util.rs:179)
-        seg_va = s.get("remote_va", 0) if int(s.get("flags", 0)) & WRITE_SEG_BY_REMOTE_VA else s.get("local_va", 0)
-        n = write_segment_count(int(seg_va), int(s["total_len"]), int(s["pmtu"]))
-        stride = int(s.get("slot_stride", slot_stride or ((int(s["pmtu"]) + 64 + 3) & ~3)))
+        if int(s.get("kind", 0)) == MSG_READ_REQUEST:
+            n = 1  # Read::handle sends one request packet (read.rs:33-89)
+        else:
+            seg_va = s.get("remote_va", 0) if int(s.get("flags", 0)) & WRITE_SEG_BY_REMOTE_VA else s.get("local_va", 0)
+            n = write_segment_count(int(seg_va), int(s["total_len"]), int(s["pmtu"]))
+        stride = int(s.get("slot_stride", slot_stride or max(128, (int(s.get("pmtu", 0)) + 64 + 3) & ~3)))
         m["npackets"], m["first_packet"], m["slot_stride"] = n, first, stride
         if "out_offset" not in s:
             m["out_offset"] = out

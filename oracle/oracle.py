@@ -296,6 +296,37 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
     icrcs = np.zeros(npk, dtype=np.uint32)
     for m in msgs:
         flags = int(m["flags"]) if "flags" in m.dtype.names else 0
+        if int(m["kind"]) == 2:  # Read::handle (read.rs:33-89): one request packet, no payload
+            assert int(m["npackets"]) == 1
+            msg = RdmaMsg()
+            msg.kind = 0
+            msg.opcode = OP_READ_REQUEST
+            msg.tran_type = int(m["tran_type"])
+            msg.solicited = 1 if flags & 0x04 else 0
+            msg.ack_req = 1 if flags & 0x08 else 0  # send_flag == IbvSendSignaled (read.rs:37)
+            msg.pkey = int(m["msn"])
+            msg.dqpn = int(m["dqpn"])
+            msg.psn = int(m["psn"])
+            msg.reth_va = int(m["remote_va"])
+            msg.reth_rkey = int(m["rkey"])
+            msg.reth_len = int(m["reth_len"])
+            msg.has_secondary_reth = 1
+            msg.sec_va = int(m["local_va"])
+            msg.sec_rkey = int(m["lkey"])
+            msg.sec_len = int(m["total_len"])
+            msg.payload = None
+            msg.payload_len = 0
+            rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]))
+            if rc or pkt.size > 0xFFFF:
+                raise ValueError(f"packet_write rc={rc}")
+            if flags & 0x01:
+                c = ipv4_checksum(pkt[:20])
+                pkt[10], pkt[11] = c >> 8, c & 0xFF
+            o = int(m["out_offset"])
+            wire[o: o + pkt.size] = pkt
+            k = int(m["first_packet"])
+            lens[k], icrcs[k] = pkt.size, int(pkt[-4:].view("<u4")[0])
+            continue
         seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])  # rust_driver utils.rs:19-33
         segs = generate_segments(seg_va, int(m["total_len"]), int(m["pmtu"]))
         assert len(segs) == int(m["npackets"])
@@ -316,6 +347,7 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
             msg.kind = 0
             msg.opcode = op
             msg.tran_type = int(m["tran_type"])
+            msg.solicited = 1 if flags & 0x04 else 0  # RdmaMessageMetaCommon::solicited
             msg.ack_req = ack
             msg.pkey = int(m["msn"])
             msg.dqpn = int(m["dqpn"])
@@ -325,7 +357,11 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
             msg.reth_len = int(m["reth_len"])
             msg.payload = payload.ctypes.data if sl else None
             msg.payload_len = sl
-            rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]))
+            rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]),
+                                   buf_len=max(8192, 128 + sl))
+            if rc == LENGTH_TOO_LONG:  # the packetizer reports length 0 and writes nothing
+                pos += sl
+                continue
             if rc:
                 raise ValueError(f"packet_write rc={rc}")
             if flags & 0x01:  # IPv4 checksum filled (responser.rs:198-201 / smoltcp fill_checksum)

@@ -67,29 +67,37 @@ def _bswap16(x: int) -> int:
 
 
 def packetizer_header_words(m, s: int) -> tuple:
-    """icrc_packetize_kernel's seg_info + build_header for segment s of message m (a
-    WRITE_MSG_DTYPE record): returns (14 LE header words, payload len, wire length L)."""
-    total, pmtu = int(m["total_len"]), int(m["pmtu"])
-    flags = int(m["flags"])
-    seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])
-    first = min(total, pmtu - (seg_va & 0xFFFFFFFF) % pmtu)
-    if s == 0:
-        start, ln = 0, first
+    """icrc_packetize_kernel's plan_packet + header_lanes for packet s of message m (a
+    WRITE_MSG_DTYPE record): returns (14 or 18 LE header words, payload len, wire length L)."""
+    kind, flags = int(m["kind"]), int(m["flags"])
+    if kind == 2:  # READ REQUEST: one packet, no payload, a secondary RETH (read.rs:57-74)
+        start, ln, hw = 0, 0, 18
     else:
-        start = first + (s - 1) * pmtu
-        ln = min(pmtu, total - start)
+        total, pmtu = int(m["total_len"]), int(m["pmtu"])
+        seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])
+        first = min(total, pmtu - (seg_va & 0xFFFFFFFF) % pmtu)
+        if s == 0:
+            start, ln = 0, first
+        else:
+            start = first + (s - 1) * pmtu
+            ln = min(pmtu, total - start)
+        hw = 14
     pad = (4 - (ln & 3)) & 3
-    L = 56 + ln + pad + 4
+    L = 4 * hw + ln + pad + 4
     n = int(m["npackets"])
     only, last = n == 1, s + 1 == n
-    if int(m["kind"]) == 0:
+    if kind == 0:
         op = 0x0A if only else (0x06 if s == 0 else (0x08 if last else 0x07))
-    else:
+        ack = 1 if (only or last) else 0
+    elif kind == 1:
         op = 0x10 if only else (0x0D if s == 0 else (0x0F if last else 0x0E))
-    ack = 1 if (only or last) else 0
+        ack = 1 if (only or last) else 0
+    else:
+        op, ack = 0x0C, 1 if flags & 0x08 else 0
+    sol = 0x80 if flags & 0x04 else 0
     psn = (int(m["psn"]) + s) & 0xFFFFFF
     va = (int(m["remote_va"]) + start) & 0xFFFFFFFFFFFFFFFF
-    w = [0] * 14
+    w = [0] * hw
     w[0] = 0x45 | (((L >> 8) & 0xFF) << 16) | ((L & 0xFF) << 24)
     w[1] = _bswap16(int(m["ip_id"]))
     w[2] = 0x1140
@@ -97,13 +105,19 @@ def packetizer_header_words(m, s: int) -> tuple:
     w[4] = _bswap32(int(m["dst_ip"]))
     w[5] = _bswap16(4791) | (_bswap16(4791) << 16)
     w[6] = _bswap16(L - 20)
-    w[7] = (((int(m["tran_type"]) << 5) & 0xFF) | op) | ((pad << 5) << 8) | (_bswap16(int(m["msn"])) << 16)
+    w[7] = (((int(m["tran_type"]) << 5) & 0xFF) | op) | ((sol | (pad << 5)) << 8) | (_bswap16(int(m["msn"])) << 16)
     w[8] = _bswap32(int(m["dqpn"]) & 0xFFFFFF)
     w[9] = _bswap32(psn) | (ack << 7)
     w[10] = _bswap32(va >> 32)
     w[11] = _bswap32(va & 0xFFFFFFFF)
     w[12] = _bswap32(int(m["rkey"]))
     w[13] = _bswap32(int(m["reth_len"]))
+    if hw == 18:
+        lva = int(m["local_va"])
+        w[14] = _bswap32(lva >> 32)
+        w[15] = _bswap32(lva & 0xFFFFFFFF)
+        w[16] = _bswap32(int(m["lkey"]))
+        w[17] = _bswap32(int(m["total_len"]))
     if flags & 0x01:
         src, dst = int(m["src_ip"]), int(m["dst_ip"])
         sm = 0x4500 + L + int(m["ip_id"]) + 0x4011 + (src >> 16) + (src & 0xFFFF) + (dst >> 16) + (dst & 0xFFFF)
@@ -111,6 +125,38 @@ def packetizer_header_words(m, s: int) -> tuple:
         sm = (sm & 0xFFFF) + (sm >> 16)
         w[2] |= _bswap16(~sm & 0xFFFF) << 16
     return tuple(w), ln, L
+
+
+def head_mask(k: np.ndarray) -> np.ndarray:
+    """icrc_device.h head_mask: OR-mask of stream word k (FF prefix, masked header bytes)."""
+    out = np.zeros(k.size, dtype=np.uint32)
+    for i, kk in enumerate(k):
+        if 0 <= kk < 16:
+            nib = (0x00000010C000D02F >> (4 * int(kk))) & 15
+            out[i] = sum(0xFF << (8 * t) for t in range(4) if nib >> t & 1)
+    return out
+
+
+def icrc_rows_aligned(img: np.ndarray, pkt: np.ndarray, rows: int = 17) -> int:
+    """The packetizer's ring slot (icrc_packetize_kernel process): the packet END-aligned in
+    `rows` rows of 64 words with leading zero rows, head masks only on the two rows holding
+    stream words 0..9, every row stepped (a zero accumulator stays zero)."""
+    L = pkt.size
+    assert L % 4 == 0
+    N = 1 + (L - 4) // 4
+    k0 = N - 64 * rows
+    assert k0 <= 0
+    lane = np.arange(64, dtype=np.int64)
+    words = np.frombuffer(pkt[: L - 4].tobytes(), "<u4")
+    j0 = (-k0) >> 6
+    acc = np.zeros(64, dtype=np.uint32)
+    for j in range(rows):
+        k = k0 + lane + 64 * j          # stream word; packet word k - 1
+        w = np.array([words[x - 1] if 1 <= x <= words.size else 0 for x in k], dtype=np.uint32)
+        u = w | (head_mask(k) if j in (j0, j0 + 1) else np.uint32(0))
+        acc = u if j == 0 else (mul_m64(img, acc) ^ u)
+    s = np.bitwise_xor.reduce(final_mul(img, acc))
+    return int(~np.uint32(s) & 0xFFFFFFFF)
 
 
 def icrc(img: np.ndarray, pkt: np.ndarray) -> int:

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 31, names
+    assert len(names) == 32, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -62,6 +62,26 @@ def test_bad_arguments_rejected_before_device():
     with pytest.raises(icrc_amd.IcrcError) as e:
         icrc_amd.compute_icrc_batch(np.zeros(100, np.uint8), [0], [10])
     assert e.value.rc == icrc_amd.EINVAL
+
+
+def test_buffers_are_not_copied_and_read_only_writes_refused():
+    """is_icrc_valid zeroes the trailer in place (packet_processor.rs:350): bytearray and
+    memoryview callers get a view of their own memory, and a read-only buffer is refused before
+    any device call instead of silently zeroing a copy."""
+    import icrc_amd
+
+    ba = bytearray(64)
+    v = icrc_amd._u8(ba, writable=True)
+    v[0] = 7
+    assert ba[0] == 7
+    mv = memoryview(ba)
+    icrc_amd._u8(mv, writable=True)[1] = 9
+    assert ba[1] == 9
+    with pytest.raises(TypeError):
+        icrc_amd.is_icrc_valid(bytes(64))
+    with pytest.raises(TypeError):
+        icrc_amd.PacketWriter(bytes(64))
+    icrc_amd._u8(bytes(64))  # read-only is fine where nothing is written
 
 
 def _crc_table():
@@ -282,6 +302,13 @@ def _packetizer_specs(rng):
              rkey=5, dqpn=4, psn=77, msn=3, dst_ip=0xC0A80003, kind=0, flags=0x03, ip_id=0xBEEF),
         dict(local_va=0x10, remote_va=0x2000, payload_offset=100, total_len=600, pmtu=256, rkey=6,
              dqpn=5, psn=0, msn=4, dst_ip=0xFFFFFFFF, src_ip=0xFFFFFFFF, kind=1, flags=0x01, ip_id=0xFFFF),
+        # READ REQUEST (read.rs:33-89), signaled and solicited, checksum filled
+        dict(local_va=0x7F1234567890, remote_va=0x7E00000000AB, total_len=0x123456, reth_len=0x123456, pmtu=4096,
+             rkey=0xAABBCCDD, lkey=0x11223344, dqpn=0xABCDEF, psn=0xFFFFFE, msn=9, dst_ip=0xC0A80003, kind=2,
+             flags=0x0D, ip_id=1),
+        dict(local_va=0, remote_va=0, total_len=0, pmtu=0, rkey=0, lkey=0, dqpn=1, psn=0, msn=0, dst_ip=1, kind=2),
+        dict(local_va=0x40, remote_va=0x80, payload_offset=8, total_len=5000, pmtu=1024, rkey=7, dqpn=6, psn=3,
+             msn=5, dst_ip=0xC0A80003, kind=0, flags=0x04, ip_id=2),
     ]
 
 
@@ -298,11 +325,16 @@ def test_packetizer_flags_change_layout_as_declared():
     assert ln == 4096 - 0xF0
 
 
+IMG64 = None
+
+
 def test_packetizer_header_formulas_match_oracle():
     """The kernel's per-word header formulas (kernel_emu.packetizer_header_words) give the bytes
     the oracle's PacketWriter restatement writes, for WRITE and READ RESPONSE messages."""
     import icrc_amd
 
+    global IMG64
+    IMG64 = icrc_amd.table_image()
     rng = np.random.default_rng(11)
     msgs = icrc_amd.write_messages(_packetizer_specs(rng))
     src = rng.integers(0, 256, 30000, dtype=np.uint8)
@@ -315,10 +347,12 @@ def test_packetizer_header_formulas_match_oracle():
             assert L == lens[k]
             o = int(m["out_offset"]) + s * int(m["slot_stride"])
             hdr = np.array(words, dtype="<u4").view(np.uint8)
-            np.testing.assert_array_equal(hdr, wire[o: o + 56])
+            np.testing.assert_array_equal(hdr, wire[o: o + hdr.size])
             pkt = wire[o: o + L]
-            assert np.all(pkt[56 + ln: L - 4] == 0)
+            assert np.all(pkt[hdr.size + ln: L - 4] == 0)
             assert oracle.compute_icrc(pkt) == icrcs[k]
+            if L <= 4352 and s % 3 == 0:  # the ring slot's row algorithm on the product's table image
+                assert kernel_emu.icrc_rows_aligned(IMG64, np.ascontiguousarray(pkt)) == icrcs[k]
 
 
 def test_rx_desc_layouts_agree():
