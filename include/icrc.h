@@ -27,7 +27,11 @@
  *     ICRC_EINVAL.
  *   - The caller owns every buffer.  Synchronous calls retain no pointer; *_device calls
  *     borrow their pointers until the stream they were issued on is synchronised.
- *   - All entry points are reentrant (per-thread streams/staging, lock-protected registry).
+ *   - All entry points are reentrant.  Scalar calls copy the packet into a pinned staging slot of
+ *     the calling thread and queue on the engine's combining submitter: concurrent callers are
+ *     merged into one launch (one thread launches, the others wait for their results).  Host
+ *     batches serialise per engine on its two pipelined staging buffers; device batches only
+ *     enqueue on the caller's stream.  The default-engine registry is lock-protected.
  *   - Every CRC is computed by the HIP kernel on the GPU; there is no CPU fallback.  With
  *     no usable GPU the calls return ICRC_ENODEV.
  */
@@ -87,7 +91,8 @@ const char *icrc_version(void);
 
 /* ---- scalar drop-ins (replace compute_icrc / is_icrc_valid) ---------------------------- */
 /* compute_icrc, packet_processor.rs:275-301.  Returns the ICRC; *err (may be NULL) gets
- * ICRC_OK or an error code (then the return value is 0). */
+ * ICRC_OK or an error code (then the return value is 0).  len in [44, 65535] (an IPv4 packet),
+ * else ICRC_EINVAL.  Latency and throughput from 1 and 3 threads: profiles/ (scalar_probe). */
 uint32_t icrc_compute(const uint8_t *pkt, size_t len, int *err);
 /* is_icrc_valid, packet_processor.rs:341-353.  *ok = 1 when the trailer matches.
  * zero_trailer != 0 reproduces the reference's in-place zeroing of the trailer (350). */

@@ -4,9 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -34,6 +36,37 @@ struct Stage {
     uint32_t i0 = 0, cnt = 0;
 };
 
+// One scalar call (icrc_compute / icrc_verify) waiting for the combining submitter.
+struct ScalarReq {
+    const uint8_t *pkt;  // the caller's packet, already copied into its thread's pinned slot
+    uint32_t len;
+    int mode;
+    uint32_t result = 0;
+    int rc = ICRC_OK;
+    bool done = false;
+};
+
+// The combining submitter: concurrent scalar calls (the emulator's send, packet-handler and
+// receive threads, packet_processor.rs:260 / udp_agent.rs:99) queue here; whichever caller finds no
+// launch in flight takes every queued call and runs them as ONE batch launch per mode (the others
+// wait on the condition variable), then hands out the results.  Packets are read by the kernel
+// straight from the callers' pinned, device-mapped staging slots (no copy engine); results come
+// back through mapped pinned memory.
+struct Combiner {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<ScalarReq *> pending;
+    bool busy = false;
+    hipStream_t stream = nullptr;
+    static constexpr uint32_t kCap = 256;  // calls per launch
+    uint64_t *h_off = nullptr;             // pinned + mapped: packet offsets from the batch base
+    uint32_t *h_len = nullptr;
+    uint32_t *h_res = nullptr;
+    uint64_t *d_off = nullptr;             // their device views
+    uint32_t *d_len = nullptr;
+    uint32_t *d_res = nullptr;
+};
+
 }  // namespace
 
 struct icrc_engine {
@@ -49,6 +82,8 @@ struct icrc_engine {
     std::mutex fork_mu;  // orders the fork / join event pair between threads
     std::mutex mu;  // guards the host-batch stages
     Stage st[2];
+    std::mutex comb_init_mu;
+    std::unique_ptr<Combiner> comb;  // scalar calls (created on first use)
 };
 
 namespace {
@@ -355,6 +390,153 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     return dispatch(e, mode, p, stream);
 }
 
+// ---- scalar drop-ins -------------------------------------------------------------------------
+// Per-thread pinned, device-mapped staging: each calling thread copies its packet into a slot of its
+// own (no lock around the copy); the slot outlives the call, one per (thread, engine).
+struct ScalarSlot {
+    const icrc_engine *engine = nullptr;
+    uint8_t *h = nullptr;  // pinned host
+    uint8_t *d = nullptr;  // device view
+    ~ScalarSlot() {
+        if (h) (void)hipHostFree(h);
+    }
+};
+constexpr size_t kScalarSlotBytes = 65536 + 64;  // any packet the C-ABI accepts (len <= 65535)
+thread_local ScalarSlot t_slot;
+
+int scalar_slot(const icrc_engine *e, uint8_t **h, uint8_t **d) {
+    if (t_slot.engine != e || !t_slot.h) {
+        if (t_slot.h) (void)hipHostFree(t_slot.h);
+        t_slot = ScalarSlot{};
+        void *p = nullptr;
+        if (hipHostMalloc(&p, kScalarSlotBytes, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+            (void)hipHostFree(p);
+            return ICRC_EDEVICE;
+        }
+        t_slot.engine = e;
+        t_slot.h = static_cast<uint8_t *>(p);
+        t_slot.d = static_cast<uint8_t *>(dp);
+    }
+    *h = t_slot.h;
+    *d = t_slot.d;
+    return ICRC_OK;
+}
+
+Combiner *combiner(icrc_engine *e, int *rc) {
+    std::lock_guard<std::mutex> lk(e->comb_init_mu);
+    if (e->comb) return e->comb.get();
+    auto c = std::make_unique<Combiner>();
+    *rc = ICRC_EDEVICE;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    void *a = nullptr, *b = nullptr, *r = nullptr;
+    if (hipHostMalloc(&a, Combiner::kCap * 8, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc(&b, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc(&r, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) {
+        *rc = ICRC_ENOMEM;
+        return nullptr;
+    }
+    c->h_off = static_cast<uint64_t *>(a);
+    c->h_len = static_cast<uint32_t *>(b);
+    c->h_res = static_cast<uint32_t *>(r);
+    void *da = nullptr, *db = nullptr, *dr = nullptr;
+    if (hipHostGetDevicePointer(&da, a, 0) != hipSuccess || hipHostGetDevicePointer(&db, b, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&dr, r, 0) != hipSuccess)
+        return nullptr;
+    c->d_off = static_cast<uint64_t *>(da);
+    c->d_len = static_cast<uint32_t *>(db);
+    c->d_res = static_cast<uint32_t *>(dr);
+    *rc = ICRC_OK;
+    e->comb = std::move(c);
+    return e->comb.get();
+}
+
+void combiner_free(icrc_engine *e) {
+    if (!e->comb) return;
+    Combiner &c = *e->comb;
+    if (c.stream) {
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipStreamDestroy(c.stream);
+    }
+    for (void *p : {static_cast<void *>(c.h_off), static_cast<void *>(c.h_len), static_cast<void *>(c.h_res)})
+        if (p) (void)hipHostFree(p);
+    e->comb.reset();
+}
+
+// One launch per mode over the taken calls (leader only, outside the combiner lock).
+void run_scalar_batch(icrc_engine *e, Combiner &c, ScalarReq *const *reqs, uint32_t n) {
+    for (int mode : {icrc::kCompute, icrc::kVerify}) {
+        uint32_t k = 0;
+        uintptr_t lo = UINTPTR_MAX;
+        for (uint32_t i = 0; i < n; i++)
+            if (reqs[i]->mode == mode) lo = std::min(lo, reinterpret_cast<uintptr_t>(reqs[i]->pkt));
+        for (uint32_t i = 0; i < n; i++) {
+            if (reqs[i]->mode != mode) continue;
+            c.h_off[k] = reinterpret_cast<uintptr_t>(reqs[i]->pkt) - lo;
+            c.h_len[k] = reqs[i]->len;
+            k++;
+        }
+        if (k == 0) continue;
+        BatchParams p{};
+        p.base = reinterpret_cast<uint8_t *>(lo);
+        p.off = c.d_off;
+        p.len = c.d_len;
+        p.n = k;
+        p.table = e->d_table;
+        p.table_quad = e->d_table_quad;
+        p.table_oct = e->d_table_oct;
+        if (mode == icrc::kCompute) p.out = c.d_res;
+        else p.ok = reinterpret_cast<uint8_t *>(c.d_res);
+        int rc = dispatch(e, mode, p, c.stream);
+        if (rc == ICRC_OK && hipStreamSynchronize(c.stream) != hipSuccess) rc = ICRC_EDEVICE;
+        k = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            if (reqs[i]->mode != mode) continue;
+            reqs[i]->rc = rc;
+            reqs[i]->result = mode == icrc::kCompute ? c.h_res[k] : reinterpret_cast<const uint8_t *>(c.h_res)[k];
+            k++;
+        }
+    }
+}
+
+int scalar_call(int mode, const uint8_t *pkt, size_t len, uint32_t *result) {
+    icrc_engine *e = nullptr;
+    int rc = icrc_engine_default(-1, &e);
+    if (rc) return rc;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    Combiner *c = combiner(e, &rc);
+    if (!c) return rc;
+    uint8_t *h = nullptr, *d = nullptr;
+    if ((rc = scalar_slot(e, &h, &d)) != ICRC_OK) return rc;
+    std::memcpy(h, pkt, len);
+    ScalarReq req;
+    req.pkt = d;
+    req.len = static_cast<uint32_t>(len);
+    req.mode = mode;
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->pending.push_back(&req);
+    while (!req.done) {
+        if (!c->busy) {  // become the leader: take every queued call, launch, hand out results
+            c->busy = true;
+            const uint32_t n = static_cast<uint32_t>(std::min<size_t>(c->pending.size(), Combiner::kCap));
+            std::vector<ScalarReq *> batch(c->pending.begin(), c->pending.begin() + n);
+            c->pending.erase(c->pending.begin(), c->pending.begin() + n);
+            lk.unlock();
+            run_scalar_batch(e, *c, batch.data(), n);
+            lk.lock();
+            for (ScalarReq *r : batch) r->done = true;
+            c->busy = false;
+            c->cv.notify_all();
+        } else {
+            c->cv.wait(lk);
+        }
+    }
+    *result = req.result;
+    return req.rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -418,6 +600,7 @@ int icrc_engine_destroy(icrc_engine *e) {
         if (e->stream) (void)hipStreamSynchronize(e->stream);
         if (e->side) (void)hipStreamSynchronize(e->side);
         for (Stage &s : e->st) stage_free(s);
+        combiner_free(e);
         if (e->d_table) (void)hipFree(e->d_table);
         if (e->d_table_quad) (void)hipFree(e->d_table_quad);
         if (e->d_table_oct) (void)hipFree(e->d_table_oct);
@@ -475,30 +658,23 @@ uint32_t icrc_compute(const uint8_t *pkt, size_t len, int *err) {
     int dummy;
     int *rc = err ? err : &dummy;
     *rc = ICRC_OK;
-    if (!pkt || len < ICRC_MIN_PACKET || len > 0xFFFFFFFFull) {
+    if (!pkt || len < ICRC_MIN_PACKET || len > 0xFFFFu) {
         *rc = ICRC_EINVAL;
         return 0;
     }
-    icrc_engine *e = nullptr;
-    if ((*rc = icrc_engine_default(-1, &e)) != ICRC_OK) return 0;
-    uint64_t off = 0;
-    uint32_t l = static_cast<uint32_t>(len);
     uint32_t out = 0;
-    *rc = host_batch(e, icrc::kCompute, const_cast<uint8_t *>(pkt), &off, &l, 1, &out, nullptr, 0);
+    *rc = scalar_call(icrc::kCompute, pkt, len, &out);
     return *rc == ICRC_OK ? out : 0;
 }
 
 int icrc_verify(uint8_t *pkt, size_t len, int zero_trailer, int *ok) {
-    if (!pkt || !ok || len < ICRC_MIN_PACKET || len > 0xFFFFFFFFull) return ICRC_EINVAL;
-    icrc_engine *e = nullptr;
-    int rc = icrc_engine_default(-1, &e);
-    if (rc) return rc;
-    uint64_t off = 0;
-    uint32_t l = static_cast<uint32_t>(len);
-    uint8_t r = 0;
-    rc = host_batch(e, icrc::kVerify, pkt, &off, &l, 1, nullptr, &r, zero_trailer);
-    if (rc == ICRC_OK) *ok = (r == ICRC_VERIFY_OK);
-    return rc;
+    if (!pkt || !ok || len < ICRC_MIN_PACKET || len > 0xFFFFu) return ICRC_EINVAL;
+    uint32_t r = 0;
+    const int rc = scalar_call(icrc::kVerify, pkt, len, &r);
+    if (rc != ICRC_OK) return rc;
+    *ok = (r == ICRC_VERIFY_OK);
+    if (zero_trailer) std::memset(pkt + len - 4, 0, 4);  // is_icrc_valid, packet_processor.rs:350
+    return ICRC_OK;
 }
 
 int icrc_compute_batch_ex(icrc_engine *e, uint8_t *base, const uint64_t *off, const uint32_t *len,

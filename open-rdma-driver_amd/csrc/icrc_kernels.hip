@@ -1016,11 +1016,16 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t *>(src) + (g.fast ? g.src : 0), 0, g.fast ? static_cast<int>((g.plen + 3u) & ~3u) : 0,
             0x00020000);
-        // payload byte offset of this lane's word: 4 pw - 4 hw (before the payload: out of range -> 0)
-        const uint32_t vb = 4u * static_cast<uint32_t>(g.k0 - 1 + static_cast<int>(lane)) - 4u * g.hw;
+        // payload byte offset of this lane's word: 4 pw - 4 hw.  Words before the payload get an
+        // explicit out-of-range offset: a wrapped negative offset plus the instruction's immediate
+        // offset zeroed the in-range lanes of a mixed 8-lane group too (measured on gfx950), so
+        // every row's offset is formed in the VGPR.
+        const int vb = 4 * (g.k0 - 1 + static_cast<int>(lane)) - 4 * static_cast<int>(g.hw);
 #pragma unroll
-        for (int j = 0; j < kRows; ++j)
-            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vb + 256u * j), 0, 0);
+        for (int j = 0; j < kRows; ++j) {
+            const int o = vb + 256 * j;
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, o >= 0 ? o : static_cast<int>(kSendOOR), 0, 0);
+        }
     };
 
     SendResults res;
@@ -1052,7 +1057,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                 const int keep = static_cast<int>(room) - 4 * pw;
                 w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
-            __builtin_amdgcn_raw_buffer_store_b32(w, os, static_cast<int>(4u * static_cast<uint32_t>(pw)), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= 0 ? 4 * pw : static_cast<int>(kSendOOR), 0, 0);
             const uint32_t uu = w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u));
             acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
         }

@@ -14,7 +14,7 @@ stop_if_fatal() {  # $1 = exit status, $2 = step name
 }
 if [ "${TESTS:-1}" = 1 ]; then
   echo "== tests"
-  timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu --maxfail=5 --timeout 300 --timeout-method thread \
     > $OUT/gpu_tests.log 2>&1; rc=$?
   tail -5 $OUT/gpu_tests.log; stop_if_fatal $rc tests
   echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?

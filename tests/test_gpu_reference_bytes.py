@@ -219,7 +219,7 @@ def test_ack_kernel_decision_and_bytes_vs_oracle(engine):
     ctx["flags"] = rng.choice([0, 1, 1, 1], n)
     for udp_only, stride in ((False, 48), (True, 20), (False, 64)):
         want, wlen = _ack_expected(desc, ctx, udp_only)
-        assert 500 < len(want) < n
+        assert 100 < len(want) < n  # ~4.5 % of the random descriptors qualify
         d_out = torch.full((n * stride,), 0xCD, dtype=torch.uint8, device="cuda")
         d_len = torch.full((n,), -1, dtype=torch.int32, device="cuda")
         engine.ack_from_rx(dev(desc.view(np.uint8)).data_ptr(), dev(ctx.view(np.uint8)).data_ptr(), n,
