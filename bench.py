@@ -293,7 +293,7 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
     return fails, checked
 
 
-PMC_TRAFFIC_FILE = "r01_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r02_pmc_traffic.json"
 
 
 def pmc_traffic(n: int, L: int):

@@ -57,6 +57,13 @@ def main():
                 d[c + "_KB_mean"] = sum(vals) / len(vals)
                 d[c + "_KB_min"] = min(vals)
                 d["dispatches_" + c] = len(vals)
+    for src in ("packetize",):
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            per = load(os.path.join(out, f"pmc_{src}_{c}", "**", "*.csv"))
+            for name, vals in per.items():
+                d = res.setdefault(src, {}).setdefault(name, {})
+                d[c + "_KB_mean"] = sum(vals) / len(vals)
+                d[c + "_KB_min"] = min(vals)
     mem = res.get("mem", {})
     known = {"flat_x4": N * L, "rows_dword": N * (L - 4), "rows_x4": N * (L - 4), "rows_chunk": N * (L - 4)}
     factors = {}
@@ -80,6 +87,27 @@ def main():
                 "fetch_correction": round(corr, 4), "fetch_bytes_corrected": round(fetch),
                 "write_bytes": round(write), "traffic_bytes": round(fetch + write),
                 "algorithmic_bytes": alg, "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
+    # the packetizer: payload read in 256-B dword rows, wire written in 256-B dword rows — the shape
+    # of membench's copy_rows (known bytes: 786432 x 4096 read, 786432 x 4152 written)
+    cp = {k: v for k, v in mem.items() if k.startswith("copy_rows<0, 0>")}
+    npk = 786432
+    for name, d in res.get("packetize", {}).items():
+        if not name.startswith("icrc_packetize_kernel") or "FETCH_SIZE_KB_mean" not in d:
+            continue
+        fc = wc = None
+        for c in cp.values():
+            if c.get("FETCH_SIZE_KB_min"):
+                fc = npk * 4096 / (c["FETCH_SIZE_KB_min"] * 1024.0)
+            if c.get("WRITE_SIZE_KB_min"):
+                wc = npk * 4152 / (c["WRITE_SIZE_KB_min"] * 1024.0)
+        fetch = d["FETCH_SIZE_KB_mean"] * 1024.0 * (fc or 2.0)
+        write = d.get("WRITE_SIZE_KB_mean", 0.0) * 1024.0 * (wc or 1.0)
+        alg = npk * (4096 + 4156 + 8)
+        res["packetize_traffic_per_launch"] = {
+            "kernel": name, "packets": npk, "fetch_correction": fc, "write_correction": wc,
+            "fetch_bytes_corrected": round(fetch), "write_bytes_corrected": round(write),
+            "traffic_bytes": round(fetch + write), "algorithmic_bytes": alg,
+            "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
     print(json.dumps(res, indent=1))
 
 

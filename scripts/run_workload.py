@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Run one workload a few times with the default dispatch (for rocprofv3 --pmc / --stats).
 
-usage: run_workload.py {c1,c2,c3,s316} [launches] [variant]   (s316: 4 Mi strided 316-byte packets)"""
+usage: run_workload.py {c1,c1w,c1vz,c2,c3,s316,packetize} [launches] [variant]
+  c1w: C1 compute with write_trailer; c1vz: C1 verify with zero_trailer; s316: 4 Mi strided
+  316-byte packets; packetize: the fused send packetizer over 192 x 16 MiB WRITE messages
+  (786 K x 4156-B packets, as bench.py --extra)"""
 import os
 import sys
 
@@ -22,12 +25,29 @@ def main():
     if len(sys.argv) > 3:
         eng.set_variant(int(sys.argv[3]))
     s = torch.cuda.current_stream().cuda_stream
-    if which in ("c1", "s316"):
-        w = workloads.write_middle_stream(1 << 20) if which == "c1" else workloads.write_middle_stream(1 << 22, pmtu=256)
+    if which in ("c1", "c1w", "c1vz", "s316"):
+        w = workloads.write_middle_stream(1 << 22, pmtu=256) if which == "s316" else workloads.write_middle_stream(1 << 20)
         L = int(w.lens[0])
         b = workloads.synthesize(eng, w, stream=s)
         out = torch.zeros(w.n, dtype=torch.int32, device="cuda")
-        fn = lambda: eng.compute_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), False, s)  # noqa: E731
+        if which == "c1vz":
+            fn = lambda: eng.verify_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), True, s)  # noqa: E731
+        else:
+            fn = lambda: eng.compute_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), which == "c1w", s)  # noqa: E731
+    elif which == "packetize":
+        nmsg, mb, pmtu = 192, 16 << 20, 4096
+        msgs = icrc_amd.write_messages([dict(local_va=0x7F0000000000 + i * mb, remote_va=0x7E0000000000 + i * mb,
+                                             payload_offset=i * mb, total_len=mb, pmtu=pmtu, rkey=3, dqpn=2 + i, psn=0,
+                                             msn=i, dst_ip=0xC0A80003, kind=0) for i in range(nmsg)],
+                                       slot_stride=56 + pmtu + 4)
+        npk = int(msgs["npackets"].sum())
+        src = torch.randint(0, 256, (nmsg * mb,), dtype=torch.uint8, device="cuda")
+        dm = torch.from_numpy(msgs.view(np.uint8)).cuda()
+        wire = torch.empty(npk * (56 + pmtu + 4), dtype=torch.uint8, device="cuda")
+        ln = torch.zeros(npk, dtype=torch.int32, device="cuda")
+        ic = torch.zeros(npk, dtype=torch.int32, device="cuda")
+        fn = lambda: eng.packetize(src.data_ptr(), src.numel(), dm.data_ptr(), nmsg, npk, wire.data_ptr(),  # noqa: E731
+                                   wire.numel(), ln.data_ptr(), ic.data_ptr(), s)
     else:
         w = workloads.mixed_mtu_stream(4 << 20) if which == "c2" else workloads.write_message(16 << 20, 4096)
         b = workloads.synthesize(eng, w, stream=s)
