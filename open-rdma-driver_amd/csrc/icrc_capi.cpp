@@ -136,12 +136,13 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     p.long_variant = e->variant >= icrc::kHybridCompactBase && hybrid_forced ? 1 : 0;
     const int short_variant = !hybrid_forced ? icrc::kDefaultRaggedVariant
                             : e->variant - (p.long_variant ? icrc::kHybridCompactBase : icrc::kHybridVariantBase);
+    const uint32_t split = icrc::split_len_for(short_variant);
     if (p.off == nullptr && p.len == nullptr) {
-        p.variant = p.ulen >= icrc::kSplitLen ? icrc::kDefaultVariant : short_variant;
+        p.variant = p.ulen >= split ? icrc::kDefaultVariant : short_variant;
         return icrc::launch_batch(mode, p, grid, stream);
     }
     p.variant = short_variant;
-    p.split_len = icrc::kSplitLen;
+    p.split_len = split;
     std::lock_guard<std::mutex> g(e->fork_mu);
     HIP_TRY(hipEventRecord(e->fork_ev, static_cast<hipStream_t>(stream)));
     HIP_TRY(hipStreamWaitEvent(e->side, e->fork_ev, 0));

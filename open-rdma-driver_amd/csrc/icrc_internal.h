@@ -52,7 +52,8 @@ struct BatchParams {
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
-constexpr int kDefaultRaggedVariant = 24;  // oct: eight packets per wavefront
+constexpr int kDefaultRaggedVariant = 40;  // oct, fixed 10-row frames (icrc_oct.hip): L <= 320
+constexpr int kOctVariant = 40;
 // Hybrid dispatch threshold: shorter packets go to the oct kernel (per-packet costs / 8), longer
 // ones to the one-packet pipeline (one contiguous row per wave instruction streams faster).
 constexpr uint32_t kSplitLen = 2048;
@@ -62,17 +63,18 @@ constexpr int kHybridVariantBase = 100;
 // receive parse (A/B against the two-pass default).
 constexpr int kHybridCompactBase = 200;
 constexpr int kRxVariantBase = 300;
-// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35 are
-// diagnostics whose results are wrong by design.
+// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35, 41, 42
+// are diagnostics whose results are wrong by design.
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 18: case 20: case 24: case 25: case 26: case 31: case 32: case 35:
+    case 40: case 41: case 42:
         return true;
     default:
         return false;
     }
 }
-inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26; }
+inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 42); }
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 
@@ -87,8 +89,14 @@ int launch_rx(const BatchParams &p, int grid, void *stream);  // fused verify + 
 // Receive parse pass 2 (the default path): descriptors from the header words, icrc_ok read from
 // p.ok where the verify pass left it.
 int launch_rx_desc(const BatchParams &p, int num_cu, void *stream);
-// Quad kernel (icrc_quad.hip), variant 19..21 (chunk size / chunks in flight).
+// Quad / chunked oct kernels (icrc_quad.hip), variants 20, 24-26 (and diagnostics 31, 32, 35).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);
+// Fixed-frame oct kernel (icrc_oct.hip), variant 40: packets of at most oct_max_len() bytes.
+int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag = 0);
+uint32_t oct_max_len();
+// The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
+// short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
+inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 2 ? oct_max_len() + 1u : kSplitLen; }
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {

@@ -1292,8 +1292,9 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 
 // Variants: 0 one packet per wave, no pipelining; 13 one chain per wave (S = 1, D = 1); 16 two
 // chains (S = 2, D = 1, the default for long packets); 15 / 18 diagnostics of the S = 1, D = 2
-// shape (loads only / CRC only: wrong results by design); 20, 24-26, 31, 32, 35: the quad / oct
-// kernels (icrc_quad.hip).
+// shape (loads only / CRC only: wrong results by design); 20, 24-26, 31, 32, 35: the quad /
+// chunked oct kernels (icrc_quad.hip); 40: the fixed-frame oct kernel (icrc_oct.hip, default
+// for short packets).
 template <int MODE>
 static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     switch (p.variant) {
@@ -1308,6 +1309,9 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 31:
     case 32:
     case 35: (void)launch_quad(MODE, p.variant, p, grid, s); break;
+    case 40: (void)launch_oct(MODE, p, grid, s); break;
+    case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
+    case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }
 }

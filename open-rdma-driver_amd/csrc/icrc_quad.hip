@@ -35,26 +35,6 @@ constexpr int kQuadEmptyE = -(1 << 30);          // word index of a group with n
 // four packets per wave read 3.7 TB/s with nt, 6.2 TB/s without (profiles/r01_membench_policy.json).
 constexpr int kQuadAux = 0;
 
-__device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
-}
-
-// XOR over each W-lane packet group (DPP quad_perm x2, then row_ror 4, 8 for W = 16 or
-// row_half_mirror for W = 8): every lane gets its group's XOR.
-template <int W>
-__device__ __forceinline__ uint32_t group_xor(uint32_t x) {
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0xB1, 0xF, 0xF, true));
-    x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x4E, 0xF, 0xF, true));
-    if constexpr (W == 16) {
-        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true));
-        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true));
-    } else {
-        static_assert(W == 8, "packet groups of 8 or 16 lanes");
-        x ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x141, 0xF, 0xF, true));
-    }
-    return x;
-}
-
 // Geometry of a W-lane packet group: G = 64 / W packets per wavefront.
 template <int W>
 struct Geo {
@@ -180,41 +160,6 @@ __device__ __forceinline__ void quad_set(const QuadBlock &B, int s, uint32_t lan
     S.rows = Rmax;
     const int full = G * s + G - 1 < nreg;
     S.hrows = full ? (Rmax - Rmin + Gm::HR < Rmax ? Rmax - Rmin + Gm::HR : Rmax) : Rmax + 1;
-}
-
-// Generic per-packet path on the W-lane tables (group 0 computes; wave-uniform result).
-template <int MODE, int W>
-__device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
-                                                     const LaneConsts &c, uint32_t lane) {
-    if (L < ICRC_MIN_PACKET) {
-        if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);
-        return MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN;
-    }
-    const uint32_t Ld = L - 4u;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
-    const uint32_t T = 4u + Ld;
-    const int z = static_cast<int>((4u - (T & 3u)) & 3u);
-    const int N = static_cast<int>((T + static_cast<uint32_t>(z)) >> 2);
-    const int R = (N + W - 1) / W;
-    const int k0 = N - W * R;
-    const int col = static_cast<int>(lane & (W - 1u));
-    const bool g0 = lane < static_cast<uint32_t>(W);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pkt, 0, aligned ? static_cast<int>(Ld) : 0, 0x00020000);
-    uint32_t acc = 0;
-    for (int r = 0; r < R; ++r) {
-        const int k = k0 + W * r + col;
-        uint32_t u;
-        if (aligned) {
-            u = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(4u * static_cast<uint32_t>(k - 1)), 0, 0);
-            u |= head_mask(k);
-        } else {
-            u = g0 ? slow_word(pkt, k, z) : 0u;
-        }
-        u = g0 ? u : 0u;
-        acc = step_m64(lds, acc, u, c);
-    }
-    const uint32_t crc = ~readlane_u32(group_xor<W>(final_mul(lds, acc, c.fin)), 0);
-    return packet_result<MODE>(p, pkt, Ld, crc, aligned, lane);
 }
 
 // Chunk pipeline.  A set's rows (end-aligned, see above) are cut into chunks of K rows, the

@@ -1,0 +1,132 @@
+// scripts/shortbench.hip — achievable HBM read bandwidth for SHORT packets (316 and 1084 bytes,
+// the 256- and 1024-byte-MTU classes of C2) by access shape: P packets per wavefront, each lane
+// loading 4 (dword) or 16 (dwordx4) bytes of a packet row, rows end-aligned to the packet like the
+// kernels, three sets of P packets in flight per wave, cache policy default or nt.  The question:
+// is the short-packet kernel's 4.3-4.8 TB/s the shape's ceiling or its own overhead?
+// Each kernel XOR-folds what it reads (no dead-code removal); the results are not ICRCs.
+// Build: hipcc --offload-arch=gfx950 -O3 -o shortbench shortbench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                 \
+        }                                                                            \
+    } while (0)
+
+constexpr uint32_t kOOR = 0x80000000u;
+
+// P packets per wave (W = 64 / P lanes each), X4: 16 bytes per lane per row, R rows per packet
+// (row bytes RB = W * (X4 ? 16 : 4), R * RB >= L), AUX load policy (0 default, 2 nt).
+template <int P, int X4, int R, int AUX>
+__global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t L, uint32_t n, uint32_t *out) {
+    constexpr int W = 64 / P;
+    constexpr int B = X4 ? 16 : 4;
+    constexpr int RB = W * B;
+    constexpr int V = X4 ? 4 : 1;
+    const uint32_t lane = threadIdx.x & 63, grp = lane / W, col = lane % W;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave;
+    const uint32_t chunk = ((n + tw - 1) / tw + 63) & ~63u;
+    const uint32_t lo = gw * chunk;
+    if (lo >= n) return;
+    const uint32_t nq = n - lo < chunk ? n - lo : chunk;
+    const uint32_t nsets = (nq + P - 1) / P;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)lo * L), 0, (int)(nq * L), 0x00020000);
+    uint32_t ua[R * V], ub[R * V], uc[R * V], acc = 0;
+    auto load = [&](uint32_t set, uint32_t(&u)[R * V]) __attribute__((always_inline)) {
+        const uint32_t q = set * P + grp;
+        const int vb = (int)(q * L + L) - R * RB + (int)(col * B);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int o = vb + RB * j;
+            const int oo = (set < nsets && o >= (int)(q * L)) ? o : (int)kOOR;
+            if constexpr (X4) {
+                auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, oo, 0, AUX);
+                u[4 * j] = v[0];
+                u[4 * j + 1] = v[1];
+                u[4 * j + 2] = v[2];
+                u[4 * j + 3] = v[3];
+            } else {
+                u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, oo, 0, AUX);
+            }
+        }
+    };
+    auto fold = [&](uint32_t(&u)[R * V]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < R * V; ++j) acc ^= u[j];
+    };
+    load(0, ua);
+    load(1, ub);
+    for (uint32_t t = 0; t < nsets; t += 3) {
+        load(t + 2, uc);
+        fold(ua);
+        load(t + 3, ua);
+        fold(ub);
+        load(t + 4, ub);
+        fold(uc);
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <class F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    uint8_t *d;
+    uint32_t *out;
+    const size_t cap = (size_t)1400 << 20;
+    CK(hipMalloc(&d, cap));
+    CK(hipMalloc(&out, 4096));
+    CK(hipMemset(d, 0x5a, cap));
+    const int reps = 20;
+    auto run = [&](const char *name, uint32_t L, uint32_t n, auto kern) {
+        float ms = time_it([&] { kern<<<cus, 1024>>>(d, L, n, out); }, reps);
+        const double bytes = (double)L * n;
+        printf("{\"L\": %u, \"shape\": \"%s\", \"ms\": %.4f, \"GB/s\": %.1f}\n", L, name, ms, bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    for (int round = 0; round < 2; ++round) {
+        const uint32_t n316 = 4u << 20, n1084 = 1u << 20;
+        run("1 pkt/wave, 256-B dword rows, default", 316, n316, short_rows<1, 0, 2, 0>);
+        run("1 pkt/wave, 256-B dword rows, nt", 316, n316, short_rows<1, 0, 2, 2>);
+        run("2 pkts/wave, 128-B dword rows, default", 316, n316, short_rows<2, 0, 3, 0>);
+        run("4 pkts/wave, 64-B dword rows, default", 316, n316, short_rows<4, 0, 5, 0>);
+        run("8 pkts/wave, 32-B dword rows, default", 316, n316, short_rows<8, 0, 10, 0>);
+        run("8 pkts/wave, 32-B dword rows, nt", 316, n316, short_rows<8, 0, 10, 2>);
+        run("4 pkts/wave, 256-B dwordx4 rows, default", 316, n316, short_rows<4, 1, 2, 0>);
+        run("8 pkts/wave, 128-B dwordx4 rows, default", 316, n316, short_rows<8, 1, 3, 0>);
+        run("8 pkts/wave, 128-B dwordx4 rows, nt", 316, n316, short_rows<8, 1, 3, 2>);
+        run("16 pkts/wave, 64-B dwordx4 rows, default", 316, n316, short_rows<16, 1, 5, 0>);
+        run("1 pkt/wave, 256-B dword rows, default", 1084, n1084, short_rows<1, 0, 5, 0>);
+        run("8 pkts/wave, 32-B dword rows, default", 1084, n1084, short_rows<8, 0, 34, 0>);
+        run("8 pkts/wave, 128-B dwordx4 rows, default", 1084, n1084, short_rows<8, 1, 9, 0>);
+        run("4 pkts/wave, 256-B dwordx4 rows, default", 1084, n1084, short_rows<4, 1, 5, 0>);
+    }
+    CK(hipFree(d));
+    CK(hipFree(out));
+    return 0;
+}

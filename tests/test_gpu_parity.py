@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 13, 16, 20, 24, 25, 26])
+@pytest.mark.parametrize("variant", [0, 13, 16, 20, 24, 25, 26, 40])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
@@ -168,7 +168,7 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [-1, 20, 24, 25, 26, 120, 124, 224])
+@pytest.mark.parametrize("variant", [-1, 20, 24, 25, 26, 40, 120, 124, 140, 224, 240])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
 def test_quad_block_transitions_compute_verify(engine, variant, n):
     """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
@@ -837,7 +837,7 @@ def test_empty_batches_are_noops(engine):
     assert icrc_amd.compute_icrc_batch(np.zeros(0, np.uint8), [], []).size == 0
 
 
-@pytest.mark.parametrize("variant", [-1, 120, 124])
+@pytest.mark.parametrize("variant", [-1, 120, 124, 140])
 @pytest.mark.parametrize("pmtu", [256, 1024])
 def test_short_strided_stream_quad_path(engine, pmtu, variant):
     """Uniform strided batches of short packets (at this size the one-packet pipeline by default;
@@ -868,7 +868,7 @@ def test_short_strided_stream_quad_path(engine, pmtu, variant):
     assert bool((d_ok == 1).all().item())
 
 
-@pytest.mark.parametrize("variant", [-1, 124])
+@pytest.mark.parametrize("variant", [-1, 124, 140])
 @pytest.mark.parametrize("n", [1, 2, 3, 5])
 def test_tiny_batches_every_path(engine, n, variant):
     """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block;
@@ -933,10 +933,10 @@ def test_split_batches_concurrent_streams(engine):
 def test_kernel_variant_validation(engine):
     import icrc_amd
 
-    for v in (-1, 0, 13, 15, 16, 18, 20, 24, 25, 26, 31, 32, 35, 120, 124, 224, 301):
+    for v in (-1, 0, 13, 15, 16, 18, 20, 24, 25, 26, 31, 32, 35, 40, 41, 42, 120, 124, 140, 142, 224, 240, 301):
         engine.set_variant(v)
     engine.set_variant(-1)
-    for v in (-2, 1, 10, 14, 19, 27, 36, 99, 100, 116, 302, 400):
+    for v in (-2, 1, 10, 14, 19, 27, 36, 43, 99, 100, 116, 143, 302, 400):
         with pytest.raises(icrc_amd.IcrcError) as e:
             engine.set_variant(v)
         assert e.value.rc == icrc_amd.EINVAL
@@ -953,6 +953,56 @@ def test_scalar_surface_accepts_any_writable_buffer():
     assert icrc_amd.is_icrc_valid(mv)
     assert bytes(mv[-4:]) == b"\0\0\0\0"
     assert icrc_amd.compute_icrc(bytes(KAT1)) == KAT1_ICRC  # read-only is fine for compute
+
+
+def test_scalar_three_threads_parity():
+    """compute_icrc / is_icrc_valid (the per-packet drop-ins, packet_processor.rs:275-301 and
+    341-353) from three host threads at once: the combining submitter folds concurrent calls into
+    one launch per mode; each caller must still get its own packet's answer, and is_icrc_valid must
+    zero exactly the caller's trailer."""
+    import threading
+
+    import icrc_amd
+
+    rng = np.random.default_rng(333)
+    jobs = []
+    for t in range(3):
+        pk = []
+        for _ in range(400):
+            L = int(rng.choice([44, 45, 47, 60, 316, 1084, 4156, 9000, 65535]))
+            pk.append(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        jobs.append(pk)
+    want = [[oracle.compute_icrc(p) for p in pk] for pk in jobs]
+    errors = []
+    barrier = threading.Barrier(3)
+
+    def worker(t):
+        try:
+            barrier.wait(timeout=60)
+            for i, p in enumerate(jobs[t]):
+                got = icrc_amd.compute_icrc(p)
+                if got != want[t][i]:
+                    errors.append(f"thread {t} compute #{i} (L={len(p)}): {got:#x} != {want[t][i]:#x}")
+                    return
+                good = bytearray(p[:-4]) + want[t][i].to_bytes(4, "little")
+                bad = bytearray(good)
+                bad[len(bad) // 2] ^= 0x10
+                if not icrc_amd.is_icrc_valid(good) or bytes(good[-4:]) != b"\0\0\0\0":
+                    errors.append(f"thread {t} verify #{i}: valid packet rejected or trailer kept")
+                    return
+                if icrc_amd.is_icrc_valid(bad):
+                    errors.append(f"thread {t} verify #{i}: corrupted packet accepted")
+                    return
+        except Exception as exc:  # noqa: BLE001
+            errors.append(f"thread {t}: {exc!r}")
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in threads), "scalar callers hung"
+    assert not errors, errors[:5]
 
 
 def test_packetize_read_requests_and_oversize(engine):

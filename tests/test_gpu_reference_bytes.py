@@ -193,7 +193,8 @@ def test_ack_kernel_reproduces_kat3(engine):
     for udp_only, want in ((False, KAT3), (True, KAT3_UDP_PAYLOAD)):
         d_out = torch.zeros(64, dtype=torch.uint8, device="cuda")
         d_len = torch.zeros(1, dtype=torch.int32, device="cuda")
-        engine.ack_from_rx(dev(desc.view(np.uint8)).data_ptr(), dev(ctx.view(np.uint8)).data_ptr(), 1, d_out.data_ptr(),
+        d_desc, d_ctx = dev(desc.view(np.uint8)), dev(ctx.view(np.uint8))  # alive until the kernel has run
+        engine.ack_from_rx(d_desc.data_ptr(), d_ctx.data_ptr(), 1, d_out.data_ptr(),
                            64, d_len.data_ptr(), udp_payload_only=udp_only, stream=stream_handle())
         torch.cuda.synchronize()
         assert int(d_len.item()) == len(want)
@@ -222,7 +223,8 @@ def test_ack_kernel_decision_and_bytes_vs_oracle(engine):
         assert 100 < len(want) < n  # ~4.5 % of the random descriptors qualify
         d_out = torch.full((n * stride,), 0xCD, dtype=torch.uint8, device="cuda")
         d_len = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-        engine.ack_from_rx(dev(desc.view(np.uint8)).data_ptr(), dev(ctx.view(np.uint8)).data_ptr(), n,
+        d_desc, d_ctx = dev(desc.view(np.uint8)), dev(ctx.view(np.uint8))  # alive until the kernel has run
+        engine.ack_from_rx(d_desc.data_ptr(), d_ctx.data_ptr(), n,
                            d_out.data_ptr(), stride, d_len.data_ptr(), udp_payload_only=udp_only,
                            stream=stream_handle())
         torch.cuda.synchronize()
@@ -263,7 +265,8 @@ def test_receive_then_ack_pipeline(engine):
     bad = int(last[3])
     d_wire.view(-1)[int(off[bad]) + 60] ^= 1  # corrupt message 3's LAST packet
     d_desc = torch.zeros(npk * 72, dtype=torch.uint8, device="cuda")
-    engine.rx_parse(d_wire.data_ptr(), dev(off).data_ptr(), d_len.data_ptr(), npk, d_desc.data_ptr(), stream=s)
+    d_off = dev(off)
+    engine.rx_parse(d_wire.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), npk, d_desc.data_ptr(), stream=s)
     # QP state per packet: message i's QP expects its LAST packet's PSN, except every 5th message
     ctx = np.zeros(npk, icrc_amd.ACK_CTX_DTYPE)
     for i, m in enumerate(msgs):
@@ -274,7 +277,8 @@ def test_receive_then_ack_pipeline(engine):
             ctx[k]["expected_psn"] = lastpsn if i % 5 else (lastpsn + 1) & 0xFFFFFF
     d_out = torch.zeros(npk * 48, dtype=torch.uint8, device="cuda")
     d_alen = torch.zeros(npk, dtype=torch.int32, device="cuda")
-    engine.ack_from_rx(d_desc.data_ptr(), dev(ctx.view(np.uint8)).data_ptr(), npk, d_out.data_ptr(), 48,
+    d_ctx = dev(ctx.view(np.uint8))
+    engine.ack_from_rx(d_desc.data_ptr(), d_ctx.data_ptr(), npk, d_out.data_ptr(), 48,
                        d_alen.data_ptr(), stream=s)
     torch.cuda.synchronize()
     alen = d_alen.cpu().numpy()
