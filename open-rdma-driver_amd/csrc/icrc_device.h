@@ -48,11 +48,21 @@ __device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const L
     return step_m64(lds, s, 0u, c);
 }
 
-// M^(64-lane)(acc) via 8 nibble lookups into this lane's private tables.
+// (a << 8) | b in one VALU op.  hipcc splits bfe-then-shift into shift + and + add (3 ops);
+// the asm keeps v_bfe_u32 + v_lshl_or_b32.
+__device__ __forceinline__ uint32_t lshl8_or(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// M^(64-lane)(acc) via 8 nibble lookups into this lane's private tables.  fin (kFinalBase +
+// lane * 4) has address bits 8..11 clear: the nibble goes there with one v_lshl_or_b32, and
+// n * 4096 rides in the ds_read offset field (2 VALU per lookup).
 __device__ __forceinline__ uint32_t final_mul(const char *lds, uint32_t acc, uint32_t fin) {
     uint32_t r[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, fin + n * 4096u + (__builtin_amdgcn_ubfe(acc, 4 * n, 4) << 8));
+    for (int n = 0; n < 8; ++n) r[n] = lds_at(lds, lshl8_or(__builtin_amdgcn_ubfe(acc, 4 * n, 4), fin) + n * 4096u);
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 

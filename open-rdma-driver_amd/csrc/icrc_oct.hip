@@ -1,27 +1,39 @@
-// icrc_oct.hip — the short-packet ICRC kernel: eight packets per wavefront, one FIXED frame of K
-// rows per set of eight (the default for packets of at most 32 K bytes; K = 10: L <= 320, the
-// 256-byte-MTU packets that dominate a mixed-MTU batch).  Bit-exact with compute_icrc /
-// is_icrc_valid (blue-rdma-device/src/third_party/net/packet_processor.rs:275-301, 341-353); the
-// algorithm is described at the top of icrc_kernels.hip.
+// icrc_oct.hip — the short-packet ICRC kernel (variant 40, the default for ragged batches and for
+// strided batches of short packets): eight packets per wavefront, each packet's rows in 10-row
+// FRAMES, frames chained for longer packets (L <= 1088 here; longer ones belong to the long-packet
+// kernel of the hybrid dispatch).  Bit-exact with compute_icrc / is_icrc_valid
+// (blue-rdma-device/src/third_party/net/packet_processor.rs:275-301, 341-353); the algorithm is
+// described at the top of icrc_kernels.hip.
 //
 // Mapping.  Lanes 8g .. 8g+7 carry one packet; a packet row is 8 stream words (one
-// buffer_load_dword per lane: 32 contiguous bytes per packet, 256 B per wave instruction); the
-// packet is END-aligned in the K-row frame, so a shorter packet has leading zero rows (a zero
-// accumulator stays zero) and the column multiplier M^(8 - c) depends only on the lane (the oct
-// table image: M^8 bulk, M^(8 - (l & 7)) final tables).
+// buffer_load_dword per lane: 32 contiguous bytes per packet, 256 B per wave instruction).  The
+// stream (N words) is front-padded with z = -N mod 8 zero words (free leading zeros), so its rows
+// are aligned to BOTH ends: lane c of row r holds word 8 r + c - z.  Hence
+//  * the header masks (stream words 0..9) always fall in rows 0..2 — three OR masks per set, read
+//    with ds_bpermute from one register that holds the mask of word k in lane k;
+//  * the column multiplier M^(8 - c) depends only on the lane (the oct table image);
+//  * a packet of R rows simply stops after its row R - 1: a set of packets with different row
+//    counts freezes each lane's accumulator past its own last row (one select per row, only in
+//    such sets), and no set ever carries leading empty rows.
 //
-// Why a fixed frame.  The previous short-packet kernel (icrc_quad.hip, kept as A/B variant 24) cut
-// each set's rows into chunks that straddle sets and blocks, so every chunk carried its own
-// bookkeeping (word index, head-mask window, last-chunk flag, trailer offset, routing) and two
-// thirds of its time on 316-byte packets went to that control.  Here a ring slot IS a set: its
-// schedule (addresses, head masks, result routing) is computed once on the load side, the process
-// side is K straight-line row steps, one final product, one group XOR and one routed result.
+// Frames.  A ring slot is one frame: the 10 row loads of one set of eight packets (rows 10 f ..
+// 10 f + 9), what the process side needs, and uniform flags (first / last frame of its set).
+// Every slot issues exactly the same loads, unconditionally (absent lanes: an out-of-range
+// offset; rows past a packet's end read what follows it, within the block, and are skipped), so
+// the compiler's vmcnt waits stay exact; the accumulator carries from frame to frame.  (A uniform
+// branch between two load sequences, tried, made it wait for all but the newest frame.)  The row loads take their row
+// offsets from the instruction's immediate field (no per-row address arithmetic; the register
+// offset is never negative, see the packetizer note in icrc_kernels.hip).
 //
-// Per 64-packet block the packets this kernel takes (44 <= L <= 32 K, 4-byte aligned, L % 4
-// == 0, within 2 GiB of the block's lowest) are sorted by row count (bitonic over the lanes), so
-// the sets are mostly uniform; a set whose packets all fill the frame masks only its first three
-// rows, any other set takes the generic per-lane mask rows.  Longer packets belong to the long-
-// packet kernel (hybrid dispatch, p.split_len); the rest go to a per-packet tail loop.
+// Why (measured, profiles/r02_shortbench.jsonl, r02_probe_short_oct_ablation.jsonl): the access
+// shape itself (8 packets per instruction, 32-B rows, default cache policy) streams at 5.96
+// TB/s on 316- and 1084-byte packets, as fast as one packet per wave; the previous kernels lost
+// to per-set instruction count (their loads-only build ran within 4 % of the full one).
+//
+// Per 64-packet block the packets this kernel takes (44 <= L <= 1088, 4-byte aligned, L % 4
+// == 0, within [-1 GiB, +1 GiB) of the block's first one) are sorted by row count (a radix sort
+// over the lanes, skipped when already sorted), so most sets are uniform.  The rest go to a
+// per-packet tail loop.
 #include <hip/hip_runtime.h>
 
 #include "icrc_device.h"
@@ -31,10 +43,13 @@ namespace icrc {
 namespace {
 
 constexpr uint32_t kOctOOR = 0x80000000u;       // buffer offset out of range: the load returns 0
+constexpr uint32_t kOctFar = 0x7FFF0000u;       // an absent lane's row offset: out of range, and
+                                                // + the immediate row offset never wraps
 constexpr uint32_t kOctRelLimit = 0x7F000000u;  // packet offset in its block + L stay below
-constexpr uint32_t kOctNotMine = 63u;           // sort key (>> 6) of a packet this phase skips
-constexpr int kOctK1 = 10, kOctK2 = 34;          // frame rows of the two phases
-constexpr uint32_t kOctMaxL = 32u * kOctK2;      // 1088: longer packets are the long-packet kernel's
+constexpr uint32_t kOctNotMine = 63u;           // sort key (>> 6) of a packet this kernel skips
+constexpr int kOctK = 10;                       // rows per frame (320 bytes of a packet)
+constexpr int kOctPairs = 2;                    // ring positions of two frames: one pair in flight
+constexpr uint32_t kOctMaxL = 1088u;            // 34 rows, 4 frames: longer packets are the long kernel's
 
 // A prepared block of 64 packets.  key / vrel / len are indexed by SORTED position (lane p);
 // pos by original index (lane i).
@@ -44,68 +59,82 @@ struct OctBlock {
     uint32_t len;   // L
     uint32_t pos;   // sorted position of packet i
     uint64_t mine;  // original indices this kernel computes
-    uint64_t boff;  // lowest offset of those packets (byte offset from p.base)
+    uint64_t boff;  // block base (byte offset from p.base): the packets' offsets are boff + vrel
+    uint32_t bend;  // highest (offset - boff + L) of those packets: the loads' record count
     int nsets;
     int block;
 };
 
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t readfirstlane_u32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v)));
+}
+
+// Maximum over the 64 lanes (DPP within 16-lane rows, then the four rows on the scalar unit).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = umax32(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0xB1, 0xF, 0xF, true)));
+    x = umax32(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x4E, 0xF, 0xF, true)));
+    x = umax32(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x124, 0xF, 0xF, true)));
+    x = umax32(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, true)));
+    const uint32_t m = umax32(umax32(readlane_u32(x, 0), readlane_u32(x, 16)), umax32(readlane_u32(x, 32), readlane_u32(x, 48)));
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));  // keep it scalar
+}
+
+// Lanes below this one whose bit is set in m.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+constexpr uint64_t kOctBaseSlack = 1ull << 30;  // block base: 1 GiB below its first packet
+
 // Classify block b from this lane's (offset, L): which packets are this kernel's, their row
-// counts, the block's base offset; sort by row count.  Returns the ballot of packets that are
-// neither this kernel's nor the long-packet kernel's (the tail loop's).
-// A phase takes the fast-path packets with LMIN < L <= 32 K (N = 1 + (L - 4) / 4 <= 8 K); the
-// fast path of the whole kernel is 44 <= L <= kOctMaxL, so both phases agree on which packets are
-// the tail loop's (and on the block base).
-template <int K, uint32_t LMIN>
-__device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B, uint64_t off, uint32_t L,
-                                              bool valid, uint32_t lo, int b, uint32_t lane) {
-    constexpr uint32_t kMaxL = 32u * K;
+// counts, the block's base offset and extent; sort by row count.  Returns the ballot of packets
+// that are neither this kernel's nor the long-packet kernel's (the tail loop's).
+__device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B, uint64_t off, uint32_t L, bool valid,
+                                              uint32_t lo, int b, uint32_t lane) {
     const bool foreign = valid && p.split_len != 0 && L >= p.split_len;  // the long-packet kernel's
-    bool fast = valid && !foreign && L >= ICRC_MIN_PACKET && L <= kOctMaxL &&
+    bool mine = valid && !foreign && L >= ICRC_MIN_PACKET && L <= kOctMaxL &&
                 ((reinterpret_cast<uintptr_t>(p.base + off) | L) & 3u) == 0;
     uint64_t boff;
     if (p.off == nullptr) {
         boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(b) * 64u) * p.stride;
-    } else {  // minimum offset over this kernel's packets (64-bit butterfly)
-        uint64_t m = fast ? off : ~0ull;
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {
-            const uint32_t pl = lane ^ static_cast<uint32_t>(s);
-            const uint64_t o = static_cast<uint64_t>(bperm(pl, static_cast<uint32_t>(m))) |
-                               (static_cast<uint64_t>(bperm(pl, static_cast<uint32_t>(m >> 32))) << 32);
-            m = o < m ? o : m;
-        }
-        boff = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(m), 0)) |
-               (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(m >> 32), 0)) << 32);
+    } else {  // 1 GiB below the first candidate's offset (packets further apart: the tail loop)
+        const uint64_t cand = __ballot(mine);
+        const int f = cand ? __builtin_ctzll(cand) : 0;
+        const uint64_t o0 = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off), f)) |
+                            (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off >> 32), f)) << 32);
+        boff = o0 > kOctBaseSlack ? o0 - kOctBaseSlack : 0ull;
     }
-    fast = fast && (off - boff) + L <= kOctRelLimit;
-    const bool mine = fast && L > LMIN && L <= kMaxL;
+    mine = mine && off >= boff && (off - boff) + L <= kOctRelLimit;
+    const uint32_t vrel = static_cast<uint32_t>(off - boff);
     const uint32_t R = mine ? (1u + ((L - 4u) >> 2) + 7u) >> 3 : kOctNotMine;
+    // sort (R << 6 | index) ascending: LSD radix over the bits of R that vary, one ballot and one
+    // ds_permute per bit (skipped when the block is already in order)
     uint32_t key = (R << 6) | lane;
     const uint32_t nxt = bperm((lane + 1u) & 63u, key);
     if (__ballot(lane == 63u || key <= nxt) != ~0ull) {
 #pragma unroll
-        for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const uint32_t other = bperm(lane ^ static_cast<uint32_t>(j), key);
-                const bool up = (lane & static_cast<uint32_t>(k)) == 0u;
-                const bool lower = (lane & static_cast<uint32_t>(j)) == 0u;
-                const uint32_t mn = key < other ? key : other;
-                const uint32_t mx = key < other ? other : key;
-                key = (lower == up) ? mn : mx;
+        for (int bit = 6; bit < 12; ++bit) {
+            const uint64_t ones = __ballot((key >> bit) & 1u);
+            if (ones != 0ull && ones != ~0ull) {
+                const uint32_t r1 = lanes_below(ones);
+                const uint32_t nzero = 64u - static_cast<uint32_t>(__popcll(ones));
+                const uint32_t dst = ((key >> bit) & 1u) ? nzero + r1 : lane - r1;
+                key = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>(dst << 2), static_cast<int>(key)));
             }
         }
     }
     const uint32_t idx = key & 63u;
     B.key = key;
-    B.vrel = bperm(idx, static_cast<uint32_t>(off - boff));
+    B.vrel = bperm(idx, vrel);
     B.len = bperm(idx, L);
     B.pos = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>(idx << 2), static_cast<int>(lane)));
     B.mine = __ballot(mine);
     B.boff = boff;
+    B.bend = wave_max_u32(mine ? vrel + L : 0u);
     B.block = b;
     B.nsets = (__popcll(B.mine) + 7) >> 3;
-    return __ballot(valid && !fast && !foreign);
+    return __ballot(valid && !mine && !foreign);
 }
 
 // The tail loop's classification (reads (offset, L) from the batch arrays).
@@ -121,33 +150,125 @@ __device__ __forceinline__ uint64_t oct_classify(const BatchParams &p, uint32_t 
         L = p.len ? p.len[i] : p.ulen;
     }
     OctBlock B;
-    return oct_block<kOctK2, 0>(p, B, off, L, valid, lo, b, lane);
+    return oct_block(p, B, off, L, valid, lo, b, lane);
 }
 
-// One ring slot: the loads of one set and what its process side needs (per-lane values in VGPRs;
-// only two uniform flags and, with trailer stores, the block base in SGPRs).
-template <int K, int MODE, bool TRAILER>
+// One ring slot = one frame of one set (per-lane values in VGPRs, flags uniform).
+template <int MODE, bool TRAILER>
 struct OctSlot {
-    uint32_t u[MODE == kVerify ? K + 1 : K];  // frame rows (+ the stored trailer, lane 8g)
-    int kf;        // stream word of this lane at frame row 0 (head masks: words 0..9)
-    uint32_t rt;   // routing: lane i of the block takes the result of lane rt (0xFF: none)
-    uint32_t tro;  // trailer offset from the block base (lane 8g of a packet), else kOctOOR
-    uint32_t rq;   // result store index (the block's packet i, after the block's last set), else kOctOOR
+    uint32_t u[MODE == kVerify ? kOctK + 1 : kOctK];  // frame rows (+ the stored trailer, lane 8g)
+    int kf;        // stream word of this lane in the set's row 0 (header masks), first frame
+    int rl;        // rows of this lane's packet from this frame's row 0 (generic sets: the freeze)
+    uint32_t rt;   // routing: lane i of the block takes the result of lane rt (0xFF: none), last frame
+    uint32_t rq;   // result store index (the block's packet i, after the block's last set), else OOR
+    uint32_t tro;  // trailer offset from the block base (lane 8g of a packet, last frame), else OOR
     uint64_t boff; // uniform (TRAILER only)
-    bool have;     // uniform: the slot holds a set
-    bool full;     // uniform: every packet of the set fills the frame (head masks on rows 0..2)
+    int rrem;      // uniform: rows of the set's longest packet from this frame's row 0
+    uint32_t fl;   // uniform flags (kOct*)
 };
+constexpr uint32_t kOctHave = 1u;   // the slot holds a frame
+constexpr uint32_t kOctFirst = 2u;  // first frame of its set
+constexpr uint32_t kOctLast = 4u;   // last frame of its set
+constexpr uint32_t kOctUni = 8u;    // every packet of the set has the same row count
+constexpr uint32_t kOctFull = 16u;  // the set's longest packet fills all rows of this frame
+
+// The row steps of one frame.  FIRST: rows 0..2 carry the header masks and row 0 starts the
+// accumulators; UNI: no per-lane freeze; FULL: all K rows (else rows past S.rrem are skipped, a
+// uniform branch per row).
+template <bool FIRST, bool UNI, bool FULL, int MODE, bool TRAILER>
+__device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm,
+                                             const char *lds, const LaneConsts &c) {
+    uint32_t m0 = 0, m1 = 0, m2 = 0;
+    if constexpr (FIRST) {
+        const uint32_t k = static_cast<uint32_t>(S.kf) & 63u;  // negative k wraps to lanes 57..63 (mask 0)
+        m0 = bperm(k, hm);
+        m1 = bperm((k + 8u) & 63u, hm);
+        m2 = bperm((k + 16u) & 63u, hm);
+    }
+#pragma unroll
+    for (int j = 0; j < kOctK; ++j) {
+        if (!FULL && j > 0 && j >= S.rrem) break;
+        uint32_t u = S.u[j];
+        if constexpr (FIRST) {
+            if (j == 0) u |= m0;
+            if (j == 1) u |= m1;
+            if (j == 2) u |= m2;
+        }
+        const uint32_t nv = (FIRST && j == 0) ? u : step_m64(lds, acc, u, c);
+        if constexpr (UNI) acc = nv;
+        else acc = j < S.rl ? nv : acc;
+    }
+    return acc;
+}
+
+// One frame's rows, dispatched on its (uniform) flags.
+template <int MODE, bool TRAILER, int DIAG>
+__device__ __forceinline__ uint32_t oct_frame(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm, const char *lds,
+                                              const LaneConsts &c) {
+    if constexpr (DIAG == 1) {
+#pragma unroll
+        for (int j = 0; j < kOctK; ++j) acc ^= S.u[j];
+        return acc;
+    } else {
+        switch (S.fl & (kOctFirst | kOctUni | kOctFull)) {
+        case kOctFirst | kOctUni | kOctFull: return oct_rows<true, true, true>(S, acc, hm, lds, c);
+        case kOctFirst | kOctFull: return oct_rows<true, false, true>(S, acc, hm, lds, c);
+        case kOctUni | kOctFull: return oct_rows<false, true, true>(S, acc, hm, lds, c);
+        case kOctFull: return oct_rows<false, false, true>(S, acc, hm, lds, c);
+        case kOctFirst | kOctUni:
+        case kOctFirst: return oct_rows<true, false, false>(S, acc, hm, lds, c);
+        default: return oct_rows<false, false, false>(S, acc, hm, lds, c);
+        }
+    }
+}
+
+// Two independent frames stepped interleaved (two accumulator chains: each row step waits on
+// LDS lookups, and the other chain's step fills that wait).  Both frames are full and uniform;
+// B is the first frame of its set, A the first (FA) or a later one.
+template <bool FA, int MODE, bool TRAILER>
+__device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const OctSlot<MODE, TRAILER> &B, uint32_t &accA,
+                                          uint32_t &accB, uint32_t hm, const char *lds, const LaneConsts &c) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0;
+    if constexpr (FA) {
+        const uint32_t k = static_cast<uint32_t>(A.kf) & 63u;
+        a0 = bperm(k, hm);
+        a1 = bperm((k + 8u) & 63u, hm);
+        a2 = bperm((k + 16u) & 63u, hm);
+    }
+    const uint32_t kb = static_cast<uint32_t>(B.kf) & 63u;
+    const uint32_t b0 = bperm(kb, hm), b1 = bperm((kb + 8u) & 63u, hm), b2 = bperm((kb + 16u) & 63u, hm);
+    uint32_t xa = accA, xb = 0;
+#pragma unroll
+    for (int j = 0; j < kOctK; ++j) {
+        uint32_t ua = A.u[j], ub = B.u[j];
+        if constexpr (FA) {
+            if (j == 0) ua |= a0;
+            if (j == 1) ua |= a1;
+            if (j == 2) ua |= a2;
+        }
+        if (j == 0) ub |= b0;
+        if (j == 1) ub |= b1;
+        if (j == 2) ub |= b2;
+        xa = (FA && j == 0) ? ua : step_m64(lds, xa, ua, c);
+        xb = j == 0 ? ub : step_m64(lds, xb, ub, c);
+    }
+    accA = xa;
+    accB = xb;
+}
 
 // DIAG (ablation builds, variants 41 / 42): 1 = the loads without the row steps and final
 // products, 2 = the row steps without the loads.
-template <int MODE, int K, int D, bool RAGGED, bool TRAILER, uint32_t LMIN, bool TAIL, int DIAG>
+template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
-    constexpr int B = D + 1;
+    constexpr int K = kOctK;
+    constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
+    constexpr int B = 2 * P;
     if (nq == 0) return;
     const int nblocks = static_cast<int>((nq + 63u) >> 6);
     const uint32_t grp = lane >> 3;
-    const uint32_t col = lane & 7u;
+    const int col = static_cast<int>(lane & 7u);
+    const uint32_t hm = head_mask(static_cast<int>(lane));  // lane k: the mask of stream word k
     bool irregular = false;
 
     // next block NB, prepared at the top of a ring cycle from the (offset, len) loaded the cycle before
@@ -156,126 +277,182 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     bool nb_ready = false;
     uint32_t m_lo = 0, m_hi = 0, m_len = 0;
 
-    // load side: the block being issued and its next set
+    // load side: the block being issued, its current set and frame
     OctBlock LB;
     LB.nsets = 0;
     LB.block = -1;
-    int lset = 0;
-    bool ldone = false;
+    LB.boff = 0;
+    LB.bend = 0;
+    int lset = 0, lf = 0, lnf = 0, lrmax = 0;
+    bool luni = true, lreal = false, ldone = false;
+    int lkf = 0, lr = 0;
+    uint32_t lvrow0 = 0, ltr = kOctOOR;
     int inflight = 0;
 
-    OctSlot<K, MODE, TRAILER> sl[B];
+    OctSlot<MODE, TRAILER> sl[B];
 #pragma unroll
-    for (int b = 0; b < B; ++b) sl[b].have = false;
+    for (int b = 0; b < B; ++b) {  // every slot's stores run from the first cycle: all out of range
+        sl[b].fl = 0u;
+        sl[b].rq = kOctOOR;
+        sl[b].tro = kOctOOR;
+        sl[b].rt = 0xFFu;
+        sl[b].boff = 0;
+    }
 
-    // process side: the block result register (lane i = packet i of the block)
-    uint32_t rbv = 0;
+    uint32_t acc_c = 0;  // accumulator carried from frame to frame
+    uint32_t rbv = 0;    // the block result register (lane i = packet i of the block)
 
     auto issue = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
-        OctSlot<K, MODE, TRAILER> &S = sl[b];
+        OctSlot<MODE, TRAILER> &S = sl[b];
         bool have = false;
         if (!ldone) {
-            if (LB.block >= 0 && lset + 1 < LB.nsets) {
-                lset += 1;
+            if (lf + 1 < lnf) {
+                lf += 1;
                 have = true;
-            } else if (nb_ready) {
-                LB = NB;
-                nb_ready = false;
-                lset = 0;
-                have = true;
-            } else if (nb_next >= nblocks) {
-                ldone = true;
-            }  // else a stall: the next block is prepared at the top of the next cycle
+            } else {
+                bool nset = false;
+                if (LB.block >= 0 && lset + 1 < LB.nsets) {
+                    lset += 1;
+                    nset = true;
+                } else if (nb_ready) {
+                    LB = NB;
+                    nb_ready = false;
+                    lset = 0;
+                    nset = true;
+                } else if (nb_next >= nblocks) {
+                    ldone = true;
+                }  // else a stall: the next block is prepared at the top of the next cycle
+                if (nset) {  // set setup: this lane's packet is sorted position 8 lset + grp
+                    const int nmine = __popcll(LB.mine);
+                    const uint32_t ps = 8u * static_cast<uint32_t>(lset) + grp;
+                    const uint32_t key = bperm(ps & 63u, LB.key);
+                    const uint32_t vrel = bperm(ps & 63u, LB.vrel);
+                    const uint32_t L = bperm(ps & 63u, LB.len);
+                    lreal = static_cast<int>(ps) < nmine;
+                    const uint32_t N = 1u + ((L - 4u) >> 2);
+                    const int z = static_cast<int>((8u - (N & 7u)) & 7u);
+                    lr = static_cast<int>(key >> 6);
+                    lkf = col - z;
+                    lvrow0 = vrel + 4u * static_cast<uint32_t>(lkf - 1);
+                    ltr = (lreal && col == 0) ? vrel + L - 4u : kOctOOR;
+                    const int lastp = 8 * lset + 7 < nmine - 1 ? 8 * lset + 7 : nmine - 1;
+                    lrmax = static_cast<int>(readlane_u32(LB.key, lastp) >> 6);
+                    luni = static_cast<int>(readlane_u32(LB.key, 8 * lset) >> 6) == lrmax;
+                    lnf = (lrmax + K - 1) / K;
+                    lf = 0;
+                    have = true;
+                }
+            }
         }
-        // this lane's packet of the set: sorted position 8 lset + grp
-        const int nmine = __popcll(LB.mine);
-        const uint32_t ps = 8u * static_cast<uint32_t>(lset) + grp;
-        const uint32_t key = bperm(ps & 63u, LB.key);
-        const uint32_t vrel = bperm(ps & 63u, LB.vrel);
-        const uint32_t L = bperm(ps & 63u, LB.len);
-        const bool real = have && static_cast<int>(ps) < nmine;
-        const int R = static_cast<int>(key >> 6);
-        const int k0 = 1 + static_cast<int>((L - 4u) >> 2) - 8 * R;  // stream word of lane 0, packet row 0
-        const int kf = k0 + static_cast<int>(col) - 8 * (K - R);      // stream word of this lane, frame row 0
-        const int vb = static_cast<int>(vrel) + 4 * (kf - 1);         // its packet word's byte offset
+        const uint32_t fo = 32u * K * static_cast<uint32_t>(lf);
+        const int rrem = lrmax - K * lf;
+        const bool live = have && lreal;
+        const uint32_t o0 = (live && lkf + 8 * K * lf >= 1) ? lvrow0 + fo : kOctOOR;
+        const uint32_t o1 = live ? lvrow0 + 32u + fo : kOctFar;  // rows >= 1: + 32 (j - 1) immediate
+        // (readfirstlane: the block fields are uniform, but hipcc's divergence analysis loses track
+        // of them through the ring's phis and wraps every load in a waterfall loop otherwise)
+        const uint64_t boff = static_cast<uint64_t>(readfirstlane_u32(static_cast<uint32_t>(LB.boff))) |
+                              (static_cast<uint64_t>(readfirstlane_u32(static_cast<uint32_t>(LB.boff >> 32))) << 32);
+        uint8_t *bb = p.base + boff;
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(p.base + LB.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc(bb, 0, static_cast<int>(readfirstlane_u32(LB.bend)), 0x00020000);
+        const bool full = rrem >= K;
+        if constexpr (DIAG == 2) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            // the full offset formed in the VGPR (no immediate offset on a lane that is out of range)
-            const int o = vb + 32 * j;
-            if constexpr (DIAG == 2) S.u[j] = static_cast<uint32_t>(o) * 0x9E3779B1u;
-            else S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(
-                rs, (real && kf + 8 * j >= 1) ? o : static_cast<int>(kOctOOR), 0, 0);
+            for (int j = 0; j < K; ++j) S.u[j] = (o1 + 32u * j) * 0x9E3779B1u;
+        } else {
+            // Rows past a packet's end read the bytes after it (bounded by the block's extent) and
+            // are never stepped: cheaper than a per-row descriptor select, and those bytes are the
+            // block's next packets (L2-resident).
+            S.u[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o0), 0, 0);
+#pragma unroll
+            for (int j = 1; j < K; ++j)
+                S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o1 + 32u * (j - 1)), 0, 0);
         }
-        const uint32_t tr = (real && col == 0u) ? vrel + L - 4u : kOctOOR;
-        if constexpr (MODE == kVerify) S.u[K] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(tr), 0, 0);
-        S.tro = tr;
-        S.kf = real ? kf : -(1 << 20);
+        const bool last = have && lf + 1 == lnf;
+        if constexpr (MODE == kVerify)
+            S.u[K] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(last ? ltr : kOctOOR), 0, 0);
+        S.kf = lkf;
+        S.rl = lr - K * lf;
+        S.rrem = rrem;
+        S.tro = last ? ltr : kOctOOR;
         // routing: packet i of the block takes group (pos_i & 7)'s result when pos_i is in this set
         const uint32_t pi = LB.pos;
         const bool mine_i = ((LB.mine >> lane) & 1ull) != 0;
-        const bool take = have && mine_i && (pi >> 3) == static_cast<uint32_t>(lset);
+        const bool take = last && mine_i && (pi >> 3) == static_cast<uint32_t>(lset);
         S.rt = take ? (pi & 7u) << 3 : 0xFFu;
-        const bool last = have && lset + 1 == LB.nsets;
-        S.rq = (last && mine_i) ? static_cast<uint32_t>(LB.block) * 64u + lane : kOctOOR;
+        S.rq = (last && lset + 1 == LB.nsets && mine_i) ? (static_cast<uint32_t>(LB.block) * 64u + lane) * (MODE == kCompute ? 4u : 1u)
+                                                        : kOctOOR;
         if constexpr (TRAILER) S.boff = LB.boff;
-        S.have = have;
-        const uint32_t rfirst = readlane_u32(LB.key, (8 * lset) & 63) >> 6;  // sorted: the set's fewest rows
-        S.full = have && rfirst == static_cast<uint32_t>(K);
+        S.fl = have ? kOctHave | (lf == 0 ? kOctFirst : 0u) | (last ? kOctLast : 0u) | (luni ? kOctUni : 0u) |
+                          (full ? kOctFull : 0u)
+                    : 0u;
         if (have) inflight += 1;
     };
 
-    auto consume = [&](auto bc) __attribute__((always_inline)) {
-        constexpr int b = decltype(bc)::value;
-        OctSlot<K, MODE, TRAILER> &S = sl[b];
-        if (!S.have) return;
-        uint32_t acc = 0;
-        if constexpr (DIAG == 1) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) acc ^= S.u[j] | head_mask(S.kf + 8 * j);
-        } else if (S.full) {  // every packet fills the frame: stream words 0..9 lie in rows 0..2
-            const uint32_t m0 = head_mask(S.kf), m1 = head_mask(S.kf + 8), m2 = head_mask(S.kf + 16);
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                uint32_t u = S.u[j];
-                if (j == 0) u |= m0;
-                if (j == 1) u |= m1;
-                if (j == 2) u |= m2;
-                acc = j == 0 ? u : step_m64(lds, acc, u, c);
-            }
-        } else {  // head masks wherever this lane's stream words 0..9 fall (branch-free, every row)
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const uint32_t u = S.u[j] | head_mask(S.kf + 8 * j);
-                acc = j == 0 ? u : step_m64(lds, acc, u, c);
-            }
-        }
-        const uint32_t crc = ~group_xor<8>(DIAG == 1 ? acc : final_mul(lds, acc, c.fin));
+    // the result of a slot's set (its last frame): ICRC / verify result, routed into rbv
+    auto finish = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
         uint32_t r;
         if constexpr (MODE == kCompute) r = crc;
         else r = bperm(grp << 3, S.u[K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+        const uint32_t v = bperm(S.rt & 63u, r);
+        rbv = S.rt != 0xFFu ? v : rbv;
+    };
+    // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
+    // around a store in the ring)
+    auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
         if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, ts, static_cast<int>(S.tro), 0, 0);
         }
-        const uint32_t v = bperm(S.rt & 63u, r);
-        rbv = S.rt != 0xFFu ? v : rbv;
-        // the block's results leave after its last set, as one store every set issues (out of range
-        // otherwise: no branch around a store in the ring)
+        // the block's results leave after its last set
         if constexpr (MODE == kCompute) {
             const __amdgpu_buffer_rsrc_t os =
                 __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0,
                                                   0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(rbv, os, static_cast<int>(S.rq == kOctOOR ? kOctOOR : 4u * S.rq), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(rbv, os, static_cast<int>(S.rq), 0, 0);
         } else {
             const __amdgpu_buffer_rsrc_t os =
                 __builtin_amdgcn_make_buffer_rsrc(p.ok ? p.ok + lo : nullptr, 0, p.ok ? static_cast<int>(nq) : 0, 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rbv), os, static_cast<int>(S.rq), 0, 0);
         }
-        inflight -= 1;
+    };
+
+    // Consume slots a (older) and a + 1.  If the second starts a new set the two frames are
+    // independent and, when both are full and uniform, stepped interleaved.
+    auto consume = [&](auto ac) __attribute__((always_inline)) {
+        constexpr int a = decltype(ac)::value;
+        OctSlot<MODE, TRAILER> &SA = sl[a];
+        OctSlot<MODE, TRAILER> &SB = sl[a + 1];
+        const uint32_t fa = SA.fl, fb = SB.fl;
+        constexpr uint32_t kFast = kOctHave | kOctUni | kOctFull;
+        uint32_t accA = acc_c, accB = 0;
+        if (DIAG != 1 && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
+            if (fa & kOctFirst) oct_rows2<true>(SA, SB, accA, accB, hm, lds, c);
+            else oct_rows2<false>(SA, SB, accA, accB, hm, lds, c);
+        } else {
+            if (fa & kOctHave) accA = oct_frame<MODE, TRAILER, DIAG>(SA, accA, hm, lds, c);
+            if (fb & kOctHave) accB = oct_frame<MODE, TRAILER, DIAG>(SB, (fb & kOctFirst) ? 0u : accA, hm, lds, c);
+        }
+        acc_c = (fb & kOctHave) ? accB : accA;
+        uint32_t crcA = 0, crcB = 0;
+        if (fa & fb & kOctLast) {  // both sets end here: the two final products interleave
+            crcA = ~group_xor<8>(DIAG == 1 ? accA : final_mul(lds, accA, c.fin));
+            crcB = ~group_xor<8>(DIAG == 1 ? accB : final_mul(lds, accB, c.fin));
+        } else if (fa & kOctLast) {
+            crcA = ~group_xor<8>(DIAG == 1 ? accA : final_mul(lds, accA, c.fin));
+        } else if (fb & kOctLast) {
+            crcB = ~group_xor<8>(DIAG == 1 ? accB : final_mul(lds, accB, c.fin));
+        }
+        inflight -= static_cast<int>(fa & kOctHave) + static_cast<int>(fb & kOctHave);
+        // A's results (and its block's result store) before B's routing touches rbv: B may hold
+        // the next block's first set
+        if (fa & kOctLast) finish(SA, crcA);
+        stores(SA, crcA);
+        if (fb & kOctLast) finish(SB, crcB);
+        stores(SB, crcB);
     };
 
     for (;;) {
@@ -290,7 +467,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                             : static_cast<uint64_t>(lo + q) * p.stride;
                 L = p.len ? m_len : p.ulen;
             }
-            if (oct_block<K, LMIN>(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
+            if (oct_block(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
             nb_next += 1;
             nb_ready = NB.nsets > 0;
         }
@@ -306,16 +483,18 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             m_len = __builtin_amdgcn_raw_buffer_load_b32(rs_len, static_cast<int>(q * 4u), 0, 0);
             mblk = nb_next;
         }
-        static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
-            constexpr int b = decltype(bc)::value;
-            issue(IntC<(b + D) % B>{});
-            consume(bc);
+        static_for<P>([&](auto pc) __attribute__((always_inline)) -> bool {
+            constexpr int q = decltype(pc)::value;
+            constexpr int n = (q + P - 1) % P;  // the pair issued now is consumed P - 1 positions later
+            issue(IntC<2 * n>{});
+            issue(IntC<2 * n + 1>{});
+            consume(IntC<2 * q>{});
             return true;
         });
         if (ldone && inflight == 0) break;
     }
 
-    if (TAIL && irregular) {  // L < 44, misaligned, L % 4 != 0, far-apart offsets: per packet
+    if (irregular) {  // L < 44, misaligned, L % 4 != 0, far-apart offsets: per packet
         for (int b = 0; b < nblocks; ++b) {
             uint64_t off;
             uint32_t L;
@@ -373,15 +552,12 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams 
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    // phase 1: L <= 320 in 10-row frames, 3 sets in flight; phase 2: 320 < L <= 1088 in 34-row
-    // frames, its 34 loads in flight before the row steps (~7.5-8.5 KiB per wave in flight either way)
-    run_oct<MODE, kOctK1, 3, RAGGED, TRAILER, 0, false, DIAG>(p, lds, c, lane, lo, nq);
-    run_oct<MODE, kOctK2, 0, RAGGED, TRAILER, 32u * kOctK1, true, DIAG>(p, lds, c, lane, lo, nq);
+    run_oct<MODE, RAGGED, TRAILER, DIAG>(p, lds, c, lane, lo, nq);
 }
 
 }  // namespace
 
-// Variant 40 (the default short-packet kernel): packets of at most 1088 bytes in two phases.
+// Variant 40 (the default short-packet kernel): packets of at most 1088 bytes.
 uint32_t oct_max_len() { return kOctMaxL; }
 
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag) {
