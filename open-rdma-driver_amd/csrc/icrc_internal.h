@@ -63,18 +63,18 @@ constexpr int kHybridVariantBase = 100;
 // receive parse (A/B against the two-pass default).
 constexpr int kHybridCompactBase = 200;
 constexpr int kRxVariantBase = 300;
-// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35, 41, 42
+// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35, 41-46
 // are diagnostics whose results are wrong by design.
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 18: case 20: case 24: case 25: case 26: case 31: case 32: case 35:
-    case 40: case 41: case 42:
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46:
         return true;
     default:
         return false;
     }
 }
-inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 42); }
+inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 46); }
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 
@@ -96,7 +96,7 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag 
 uint32_t oct_max_len();
 // The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
 // short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
-inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 2 ? oct_max_len() + 1u : kSplitLen; }
+inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 6 ? oct_max_len() + 1u : kSplitLen; }
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {

@@ -1312,6 +1312,10 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 40: (void)launch_oct(MODE, p, grid, s); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
+    case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products
+    case 44: (void)launch_oct(MODE, p, grid, s, 4); break;  // diagnostic: control only
+    case 45: (void)launch_oct(MODE, p, grid, s, 5); break;  // diagnostic: loads only, no stores
+    case 46: (void)launch_oct(MODE, p, grid, s, 6); break;  // diagnostic: no per-frame stores
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }
 }

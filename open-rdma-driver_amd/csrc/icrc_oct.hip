@@ -48,20 +48,33 @@ constexpr uint32_t kOctFar = 0x7FFF0000u;       // an absent lane's row offset: 
 constexpr uint32_t kOctRelLimit = 0x7F000000u;  // packet offset in its block + L stay below
 constexpr uint32_t kOctNotMine = 63u;           // sort key (>> 6) of a packet this kernel skips
 constexpr int kOctK = 10;                       // rows per frame (320 bytes of a packet)
+constexpr bool kOctPrio = true;
 constexpr int kOctPairs = 2;                    // ring positions of two frames: one pair in flight
 constexpr uint32_t kOctMaxL = 1088u;            // 34 rows, 4 frames: longer packets are the long kernel's
 
+// Frame descriptor (one per frame of a block, lane t of OctBlock::ftab; also the slot flags):
+constexpr uint32_t kFdSet = 7u;             // bits 0-2: the set (sorted positions 8 s .. 8 s + 7)
+constexpr uint32_t kOctFirst = 1u << 3;     // first frame of its set
+constexpr uint32_t kOctLast = 1u << 4;      // last frame of its set
+constexpr uint32_t kOctUni = 1u << 5;       // every packet of the set has the same row count
+constexpr uint32_t kOctFull = 1u << 6;      // the set's longest packet fills all rows of this frame
+constexpr uint32_t kOctBlockLast = 1u << 7; // last frame of the block: its results leave
+constexpr uint32_t kOctHave = 1u << 8;      // (slot flags) the slot holds a frame
+// bits 16-23: frame index f in the set; bits 24-31: rows of the set's longest packet from the
+// frame's row 0 (rrem)
+
 // A prepared block of 64 packets.  key / vrel / len are indexed by SORTED position (lane p);
-// pos by original index (lane i).
+// pos by original index (lane i); ftab by frame (lane t).
 struct OctBlock {
     uint32_t key;   // R << 6 | original index (R = kOctNotMine: not this kernel's)
     uint32_t vrel;  // packet offset - boff
     uint32_t len;   // L
     uint32_t pos;   // sorted position of packet i
+    uint32_t ftab;  // frame descriptors
     uint64_t mine;  // original indices this kernel computes
     uint64_t boff;  // block base (byte offset from p.base): the packets' offsets are boff + vrel
     uint32_t bend;  // highest (offset - boff + L) of those packets: the loads' record count
-    int nsets;
+    int nfr;        // frames
     int block;
 };
 
@@ -129,11 +142,40 @@ __device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B,
     B.vrel = bperm(idx, vrel);
     B.len = bperm(idx, L);
     B.pos = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>(idx << 2), static_cast<int>(lane)));
+    B.pos = mine ? B.pos : 0xFFu;
     B.mine = __ballot(mine);
     B.boff = boff;
     B.bend = wave_max_u32(mine ? vrel + L : 0u);
     B.block = b;
-    B.nsets = (__popcll(B.mine) + 7) >> 3;
+    // The frame schedule.  Lane s < nsets: set s's longest / shortest row count and frame count
+    // (ceil(R / 10) as a multiply-shift, exact below 2000), and its first frame (a DPP prefix sum
+    // over lanes 0..7); then every frame lane t finds its set through a scattered start mark.
+    const int nmine = __popcll(B.mine);
+    const uint32_t nsets = static_cast<uint32_t>((nmine + 7) >> 3);
+    const uint32_t s8 = (lane & 7u) * 8u;
+    const uint32_t plast = s8 + 7u < static_cast<uint32_t>(nmine - 1) ? s8 + 7u : static_cast<uint32_t>(nmine - 1);
+    const uint32_t rmax = bperm(plast & 63u, key) >> 6;
+    const uint32_t rmin = bperm(s8, key) >> 6;
+    const bool live_set = lane < nsets;
+    const uint32_t nf = live_set ? ((rmax + 9u) * 6554u) >> 16 : 0u;
+    uint32_t inc = nf;  // inclusive prefix sum within the first DPP row (lanes 0..15)
+    inc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(inc), 0x111, 0xF, 0xF, true));
+    inc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(inc), 0x112, 0xF, 0xF, true));
+    inc += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(inc), 0x114, 0xF, 0xF, true));
+    const uint32_t start = inc - nf;
+    B.nfr = nsets ? static_cast<int>(readlane_u32(inc, 7)) : 0;
+    const uint32_t sinfo = start | (nf << 8) | (rmax << 16) | (rmin == rmax ? 1u << 24 : 0u);
+    const uint32_t mark = static_cast<uint32_t>(__builtin_amdgcn_ds_permute(static_cast<int>((live_set ? start : 63u) << 2),
+                                                                            static_cast<int>(live_set ? 1u : 0u)));
+    const uint64_t starts = __ballot(mark != 0u);
+    const uint32_t st = lanes_below(starts) + static_cast<uint32_t>((starts >> lane) & 1ull) - 1u;  // this frame's set
+    const uint32_t si = bperm(st & 7u, sinfo);
+    const uint32_t f = lane - (si & 0xFFu);
+    const uint32_t rrem = ((si >> 16) & 0xFFu) - static_cast<uint32_t>(kOctK) * f;
+    B.ftab = (st & kFdSet) | (f == 0u ? kOctFirst : 0u) | (f + 1u == ((si >> 8) & 0xFFu) ? kOctLast : 0u) |
+             ((si >> 24) ? kOctUni : 0u) | (rrem >= static_cast<uint32_t>(kOctK) ? kOctFull : 0u) |
+             (static_cast<int>(lane) + 1 == B.nfr ? kOctBlockLast : 0u) | kOctHave | (f << 16) |
+             ((rrem < 255u ? rrem : 255u) << 24);
     return __ballot(valid && !mine && !foreign);
 }
 
@@ -153,24 +195,18 @@ __device__ __forceinline__ uint64_t oct_classify(const BatchParams &p, uint32_t 
     return oct_block(p, B, off, L, valid, lo, b, lane);
 }
 
-// One ring slot = one frame of one set (per-lane values in VGPRs, flags uniform).
+// One ring slot = one frame of one set (per-lane values in VGPRs, the frame descriptor in an SGPR).
 template <int MODE, bool TRAILER>
 struct OctSlot {
     uint32_t u[MODE == kVerify ? kOctK + 1 : kOctK];  // frame rows (+ the stored trailer, lane 8g)
     int kf;        // stream word of this lane in the set's row 0 (header masks), first frame
     int rl;        // rows of this lane's packet from this frame's row 0 (generic sets: the freeze)
     uint32_t rt;   // routing: lane i of the block takes the result of lane rt (0xFF: none), last frame
-    uint32_t rq;   // result store index (the block's packet i, after the block's last set), else OOR
+    uint32_t rq;   // result store offset (the block's packet i, block's last frame), else OOR
     uint32_t tro;  // trailer offset from the block base (lane 8g of a packet, last frame), else OOR
     uint64_t boff; // uniform (TRAILER only)
-    int rrem;      // uniform: rows of the set's longest packet from this frame's row 0
-    uint32_t fl;   // uniform flags (kOct*)
+    uint32_t fl;   // uniform: the frame descriptor (kOct* flags, rrem in bits 24-31), 0 if empty
 };
-constexpr uint32_t kOctHave = 1u;   // the slot holds a frame
-constexpr uint32_t kOctFirst = 2u;  // first frame of its set
-constexpr uint32_t kOctLast = 4u;   // last frame of its set
-constexpr uint32_t kOctUni = 8u;    // every packet of the set has the same row count
-constexpr uint32_t kOctFull = 16u;  // the set's longest packet fills all rows of this frame
 
 // The row steps of one frame.  FIRST: rows 0..2 carry the header masks and row 0 starts the
 // accumulators; UNI: no per-lane freeze; FULL: all K rows (else rows past S.rrem are skipped, a
@@ -187,7 +223,7 @@ __device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, ui
     }
 #pragma unroll
     for (int j = 0; j < kOctK; ++j) {
-        if (!FULL && j > 0 && j >= S.rrem) break;
+        if (!FULL && j > 0 && j >= static_cast<int>(S.fl >> 24)) break;
         uint32_t u = S.u[j];
         if constexpr (FIRST) {
             if (j == 0) u |= m0;
@@ -205,7 +241,7 @@ __device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, ui
 template <int MODE, bool TRAILER, int DIAG>
 __device__ __forceinline__ uint32_t oct_frame(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm, const char *lds,
                                               const LaneConsts &c) {
-    if constexpr (DIAG == 1) {
+    if constexpr (DIAG == 1 || DIAG == 3 || DIAG == 4 || DIAG == 5) {
 #pragma unroll
         for (int j = 0; j < kOctK; ++j) acc ^= S.u[j];
         return acc;
@@ -256,8 +292,10 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
     accB = xb;
 }
 
-// DIAG (ablation builds, variants 41 / 42): 1 = the loads without the row steps and final
-// products, 2 = the row steps without the loads.
+// DIAG (ablation builds, variants 41-46): 1 = the loads without the row steps and final
+// products, 2 = the row steps without the loads, 3 = neither loads nor row steps (control and
+// final products), 4 = control only, 5 = 1 without the per-frame stores, 6 = the full kernel
+// without the per-frame stores.
 template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
@@ -277,14 +315,16 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     bool nb_ready = false;
     uint32_t m_lo = 0, m_hi = 0, m_len = 0;
 
-    // load side: the block being issued, its current set and frame
+    // load side: the block being issued (LB), its next frame (lt of lnfr) and the current set's
+    // per-lane data (set up at the set's first frame)
     OctBlock LB;
-    LB.nsets = 0;
-    LB.block = -1;
+    LB.nfr = 0;
+    LB.block = 0;
     LB.boff = 0;
     LB.bend = 0;
-    int lset = 0, lf = 0, lnf = 0, lrmax = 0;
-    bool luni = true, lreal = false, ldone = false;
+    LB.pos = 0xFFu;
+    int lt = 0, lnfr = 0;
+    bool lreal = false, ldone = false;
     int lkf = 0, lr = 0;
     uint32_t lvrow0 = 0, ltr = kOctOOR;
     int inflight = 0;
@@ -305,50 +345,36 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     auto issue = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
         OctSlot<MODE, TRAILER> &S = sl[b];
-        bool have = false;
-        if (!ldone) {
-            if (lf + 1 < lnf) {
-                lf += 1;
-                have = true;
-            } else {
-                bool nset = false;
-                if (LB.block >= 0 && lset + 1 < LB.nsets) {
-                    lset += 1;
-                    nset = true;
-                } else if (nb_ready) {
-                    LB = NB;
-                    nb_ready = false;
-                    lset = 0;
-                    nset = true;
-                } else if (nb_next >= nblocks) {
-                    ldone = true;
-                }  // else a stall: the next block is prepared at the top of the next cycle
-                if (nset) {  // set setup: this lane's packet is sorted position 8 lset + grp
-                    const int nmine = __popcll(LB.mine);
-                    const uint32_t ps = 8u * static_cast<uint32_t>(lset) + grp;
-                    const uint32_t key = bperm(ps & 63u, LB.key);
-                    const uint32_t vrel = bperm(ps & 63u, LB.vrel);
-                    const uint32_t L = bperm(ps & 63u, LB.len);
-                    lreal = static_cast<int>(ps) < nmine;
-                    const uint32_t N = 1u + ((L - 4u) >> 2);
-                    const int z = static_cast<int>((8u - (N & 7u)) & 7u);
-                    lr = static_cast<int>(key >> 6);
-                    lkf = col - z;
-                    lvrow0 = vrel + 4u * static_cast<uint32_t>(lkf - 1);
-                    ltr = (lreal && col == 0) ? vrel + L - 4u : kOctOOR;
-                    const int lastp = 8 * lset + 7 < nmine - 1 ? 8 * lset + 7 : nmine - 1;
-                    lrmax = static_cast<int>(readlane_u32(LB.key, lastp) >> 6);
-                    luni = static_cast<int>(readlane_u32(LB.key, 8 * lset) >> 6) == lrmax;
-                    lnf = (lrmax + K - 1) / K;
-                    lf = 0;
-                    have = true;
-                }
-            }
+        if (lt >= lnfr) {  // the block is issued: the next one, if prepared
+            if (nb_ready) {
+                LB = NB;
+                nb_ready = false;
+                lt = 0;
+                lnfr = LB.nfr;
+            } else if (nb_next >= nblocks) {
+                ldone = true;
+            }  // else a stall: the next block is prepared at the top of the next cycle
         }
-        const uint32_t fo = 32u * K * static_cast<uint32_t>(lf);
-        const int rrem = lrmax - K * lf;
+        const bool have = lt < lnfr;
+        const uint32_t fd = have ? readfirstlane_u32(readlane_u32(LB.ftab, lt)) : 0u;
+        const uint32_t set = fd & kFdSet;
+        if (fd & kOctFirst) {  // set setup: this lane's packet is sorted position 8 set + grp
+            const uint32_t ps = 8u * set + grp;
+            const uint32_t key = bperm(ps, LB.key);
+            const uint32_t vrel = bperm(ps, LB.vrel);
+            const uint32_t L = bperm(ps, LB.len);
+            lreal = ps < static_cast<uint32_t>(__popcll(LB.mine));
+            const uint32_t N = 1u + ((L - 4u) >> 2);
+            const int z = static_cast<int>((8u - (N & 7u)) & 7u);
+            lr = static_cast<int>(key >> 6);
+            lkf = col - z;
+            lvrow0 = vrel + 4u * static_cast<uint32_t>(lkf - 1);
+            ltr = (lreal && col == 0) ? vrel + L - 4u : kOctOOR;
+        }
+        const uint32_t lf = (fd >> 16) & 0xFFu;
+        const uint32_t fo = 32u * K * lf;
         const bool live = have && lreal;
-        const uint32_t o0 = (live && lkf + 8 * K * lf >= 1) ? lvrow0 + fo : kOctOOR;
+        const uint32_t o0 = (live && lkf + 8 * K * static_cast<int>(lf) >= 1) ? lvrow0 + fo : kOctOOR;
         const uint32_t o1 = live ? lvrow0 + 32u + fo : kOctFar;  // rows >= 1: + 32 (j - 1) immediate
         // (readfirstlane: the block fields are uniform, but hipcc's divergence analysis loses track
         // of them through the ring's phis and wraps every load in a waterfall loop otherwise)
@@ -357,38 +383,36 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         uint8_t *bb = p.base + boff;
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(bb, 0, static_cast<int>(readfirstlane_u32(LB.bend)), 0x00020000);
-        const bool full = rrem >= K;
-        if constexpr (DIAG == 2) {
+        if constexpr (DIAG >= 2 && DIAG <= 4) {
 #pragma unroll
             for (int j = 0; j < K; ++j) S.u[j] = (o1 + 32u * j) * 0x9E3779B1u;
         } else {
             // Rows past a packet's end read the bytes after it (bounded by the block's extent) and
             // are never stepped: cheaper than a per-row descriptor select, and those bytes are the
             // block's next packets (L2-resident).
+            if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(3);  // the loads go out ahead of other waves' ALU work
             S.u[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o0), 0, 0);
 #pragma unroll
             for (int j = 1; j < K; ++j)
                 S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o1 + 32u * (j - 1)), 0, 0);
+            if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(0);
         }
-        const bool last = have && lf + 1 == lnf;
+        const bool last = (fd & kOctLast) != 0u;
         if constexpr (MODE == kVerify)
             S.u[K] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(last ? ltr : kOctOOR), 0, 0);
         S.kf = lkf;
-        S.rl = lr - K * lf;
-        S.rrem = rrem;
+        S.rl = lr - K * static_cast<int>(lf);
         S.tro = last ? ltr : kOctOOR;
-        // routing: packet i of the block takes group (pos_i & 7)'s result when pos_i is in this set
+        // routing: packet i of the block (pos_i = its sorted position, 0xFF if not this kernel's)
+        // takes group (pos_i & 7)'s result at the last frame of set pos_i >> 3
         const uint32_t pi = LB.pos;
-        const bool mine_i = ((LB.mine >> lane) & 1ull) != 0;
-        const bool take = last && mine_i && (pi >> 3) == static_cast<uint32_t>(lset);
-        S.rt = take ? (pi & 7u) << 3 : 0xFFu;
-        S.rq = (last && lset + 1 == LB.nsets && mine_i) ? (static_cast<uint32_t>(LB.block) * 64u + lane) * (MODE == kCompute ? 4u : 1u)
-                                                        : kOctOOR;
-        if constexpr (TRAILER) S.boff = LB.boff;
-        S.fl = have ? kOctHave | (lf == 0 ? kOctFirst : 0u) | (last ? kOctLast : 0u) | (luni ? kOctUni : 0u) |
-                          (full ? kOctFull : 0u)
-                    : 0u;
-        if (have) inflight += 1;
+        S.rt = (last && (pi >> 3) == set) ? (pi & 7u) << 3 : 0xFFu;
+        S.rq = ((fd & kOctBlockLast) && pi != 0xFFu) ? (static_cast<uint32_t>(LB.block) * 64u + lane) * (MODE == kCompute ? 4u : 1u)
+                                                    : kOctOOR;
+        if constexpr (TRAILER) S.boff = boff;
+        S.fl = fd;
+        lt += have ? 1 : 0;
+        inflight += have ? 1 : 0;
     };
 
     // the result of a slot's set (its last frame): ICRC / verify result, routed into rbv
@@ -402,12 +426,14 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
     // around a store in the ring)
     auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
-        if constexpr (TRAILER) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
+        if constexpr (DIAG >= 5) return;
+        if (TRAILER && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, ts, static_cast<int>(S.tro), 0, 0);
         }
         // the block's results leave after its last set
+        if (!(S.fl & kOctBlockLast)) return;
         if constexpr (MODE == kCompute) {
             const __amdgpu_buffer_rsrc_t os =
                 __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0,
@@ -429,7 +455,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         const uint32_t fa = SA.fl, fb = SB.fl;
         constexpr uint32_t kFast = kOctHave | kOctUni | kOctFull;
         uint32_t accA = acc_c, accB = 0;
-        if (DIAG != 1 && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
+        if ((DIAG == 0 || DIAG == 2 || DIAG == 6) && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
             if (fa & kOctFirst) oct_rows2<true>(SA, SB, accA, accB, hm, lds, c);
             else oct_rows2<false>(SA, SB, accA, accB, hm, lds, c);
         } else {
@@ -439,14 +465,14 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         acc_c = (fb & kOctHave) ? accB : accA;
         uint32_t crcA = 0, crcB = 0;
         if (fa & fb & kOctLast) {  // both sets end here: the two final products interleave
-            crcA = ~group_xor<8>(DIAG == 1 ? accA : final_mul(lds, accA, c.fin));
-            crcB = ~group_xor<8>(DIAG == 1 ? accB : final_mul(lds, accB, c.fin));
+            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accA : final_mul(lds, accA, c.fin));
+            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accB : final_mul(lds, accB, c.fin));
         } else if (fa & kOctLast) {
-            crcA = ~group_xor<8>(DIAG == 1 ? accA : final_mul(lds, accA, c.fin));
+            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accA : final_mul(lds, accA, c.fin));
         } else if (fb & kOctLast) {
-            crcB = ~group_xor<8>(DIAG == 1 ? accB : final_mul(lds, accB, c.fin));
+            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accB : final_mul(lds, accB, c.fin));
         }
-        inflight -= static_cast<int>(fa & kOctHave) + static_cast<int>(fb & kOctHave);
+        inflight -= ((fa & kOctHave) ? 1 : 0) + ((fb & kOctHave) ? 1 : 0);
         // A's results (and its block's result store) before B's routing touches rbv: B may hold
         // the next block's first set
         if (fa & kOctLast) finish(SA, crcA);
@@ -455,6 +481,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         stores(SB, crcB);
     };
 
+    int cycles = 0;
     for (;;) {
         // top of the cycle: prepare the next block, then fetch the (offset, len) of the one after
         if (!nb_ready && nb_next < nblocks && (!RAGGED || mblk == nb_next)) {
@@ -469,7 +496,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             }
             if (oct_block(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
             nb_next += 1;
-            nb_ready = NB.nsets > 0;
+            nb_ready = NB.nfr > 0;
         }
         if constexpr (RAGGED) {  // unconditional: one load pair per cycle keeps vmcnt exact
             const uint32_t q = static_cast<uint32_t>(nb_next) * 64u + lane;
@@ -492,6 +519,9 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             return true;
         });
         if (ldone && inflight == 0) break;
+        // Safety net: a block needs at most 32 frames (8 cycles of 2 P slots) plus a stall cycle;
+        // a bookkeeping bug must end in wrong results, never in waves that do not finish.
+        if (++cycles > 12 * nblocks + 16) break;
     }
 
     if (irregular) {  // L < 44, misaligned, L % 4 != 0, far-apart offsets: per packet
@@ -564,16 +594,22 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool ragged = p.off != nullptr || p.len != nullptr;
 #define ICRC_O(M, R, T, G) hipLaunchKernelGGL((icrc_oct_kernel<M, R, T, G>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_OD(M, R)                                                \
+    do {                                                             \
+        switch (diag) {                                              \
+        case 1: ICRC_O(M, R, false, 1); break;                       \
+        case 2: ICRC_O(M, R, false, 2); break;                       \
+        case 3: ICRC_O(M, R, false, 3); break;                       \
+        case 4: ICRC_O(M, R, false, 4); break;                       \
+        case 5: ICRC_O(M, R, false, 5); break;                       \
+        default: ICRC_O(M, R, false, 6); break;                      \
+        }                                                            \
+    } while (0)
 #define ICRC_OM(M)                                                   \
     do {                                                             \
         if (diag != 0 && M == kCompute && !p.trailer) {              \
-            if (ragged) {                                            \
-                if (diag == 1) ICRC_O(M, true, false, 1);            \
-                else ICRC_O(M, true, false, 2);                      \
-            } else {                                                 \
-                if (diag == 1) ICRC_O(M, false, false, 1);           \
-                else ICRC_O(M, false, false, 2);                     \
-            }                                                        \
+            if (ragged) ICRC_OD(M, true);                            \
+            else ICRC_OD(M, false);                                  \
         } else if (ragged) {                                         \
             if (p.trailer) ICRC_O(M, true, true, 0);                 \
             else ICRC_O(M, true, false, 0);                          \
@@ -585,6 +621,7 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
     if (mode == kCompute) ICRC_OM(kCompute);
     else ICRC_OM(kVerify);
 #undef ICRC_OM
+#undef ICRC_OD
 #undef ICRC_O
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
