@@ -422,6 +422,9 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 // streams from HBM at ~6.2 TB/s, while four packets per instruction stop at ~4.5 TB/s
 // (profiles/r01_membench.json, patterns D and E).  The walk skips short packets with the
 // ballot of each 64-packet meta block; results are kept per block and stored 64 at a time.
+// Packets in flight ahead of the one being stepped (3 measured the same on C2: the long half's
+// tail is the CUs freeing up from the short-packet kernel, not the walk's latency).
+constexpr int kLongWalkDepth = 1;
 template <int MODE, int D, int ABL, bool TRAILER>
 __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
                                                    uint32_t lane, uint32_t lo, uint32_t nq) {
@@ -536,7 +539,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
     if constexpr (COMPACT) {
-        run_pipelined_long<MODE, 1, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+        run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
     } else {
         // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
         // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
             run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
         else
-            run_pipelined_long<MODE, 1, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+            run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
     }
 }
 
