@@ -28,7 +28,7 @@ constexpr uint32_t kOOR = 0x80000000u;
 // (8 / 16 / 32 lanes); 7 the trailers of a 64-packet block stored together at its end, one
 // scattered store instruction (lane q -> packet q's trailer); AUX = cache policy bits of the
 // buffer store (0 default, 2 nt); LAUX = row-load policy (2 nt, 0 default).
-template <int SHAPE, int AUX, int LAUX = 2>
+template <int SHAPE, int AUX, int LAUX = 2, int LLAST = -1>
 __global__ __launch_bounds__(1024) void rows_trailer(uint8_t *base, uint32_t *out) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -46,7 +46,8 @@ __global__ __launch_bounds__(1024) void rows_trailer(uint8_t *base, uint32_t *ou
     auto load = [&](uint32_t q, uint32_t (&u)[17]) {
         auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)(lo + q) * kL), 0, (int)(kL - 4), 0x00020000);
 #pragma unroll
-        for (int j = 0; j < 17; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 256u * j), 0, LAUX);
+        for (int j = 0; j < 16; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 256u * j), 0, LAUX);
+        u[16] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(vb + 256u * 16), 0, LLAST >= 0 ? LLAST : LAUX);
     };
     auto fold = [&](uint32_t q, uint32_t (&u)[17]) {
         uint32_t a = 0;
@@ -133,6 +134,15 @@ int main() {
     for (int round = 0; round < 1; ++round) {
 #define RUN(S, A, NAME) report(NAME, time_it([&] { rows_trailer<S, A><<<cus, 1024>>>(d, out); }, reps))
         RUN(0, 0, "T0 rows, no trailer store");
+        report("T8 default-policy loads + 4-B buffer store",
+               time_it([&] { rows_trailer<2, 0, 0><<<cus, 1024>>>(d, out); }, reps));
+        report("T9 nt loads but the trailer's row default policy + 4-B buffer store",
+               time_it([&] { rows_trailer<2, 0, 2, 0><<<cus, 1024>>>(d, out); }, reps));
+        report("T10 rows (nt, no store) then the separate trailer pass, both timed (cold trailer lines)",
+               time_it([&] {
+                   rows_trailer<0, 0><<<cus, 1024>>>(d, out);
+                   trailer_pass<<<(kN + 255) / 256, 256>>>(d, kN);
+               }, reps));
         report("T0d rows, no trailer store, default-policy loads",
                time_it([&] { rows_trailer<0, 0, 0><<<cus, 1024>>>(d, out); }, reps));
         RUN(7, 0, "T7 trailers of 64 packets in one scattered store at the block end");
