@@ -23,7 +23,7 @@ constexpr uint32_t kOOR = 0x80000000u;
 
 // P packets per wave (W = 64 / P lanes each), X4: 16 bytes per lane per row, R rows per packet
 // (row bytes RB = W * (X4 ? 16 : 4), R * RB >= L), AUX load policy (0 default, 2 nt).
-template <int P, int X4, int R, int AUX>
+template <int P, int X4, int R, int AUX, int WORK = 0>
 __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t L, uint32_t n, uint32_t *out) {
     constexpr int W = 64 / P;
     constexpr int B = X4 ? 16 : 4;
@@ -62,6 +62,9 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
     auto fold = [&](uint32_t(&u)[R * V]) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < R * V; ++j) acc ^= u[j];
+        // WORK dependent VALU ops per set (a stand-in for the CRC's per-set instruction count)
+#pragma unroll
+        for (int w = 0; w < WORK; ++w) acc = __builtin_amdgcn_perm(acc, acc + static_cast<uint32_t>(w), 0x05040302u + w);
     };
     load(0, ua);
     load(1, ub);
@@ -121,6 +124,10 @@ int main() {
         run("8 pkts/wave, 128-B dwordx4 rows, default", 316, n316, short_rows<8, 1, 3, 0>);
         run("8 pkts/wave, 128-B dwordx4 rows, nt", 316, n316, short_rows<8, 1, 3, 2>);
         run("16 pkts/wave, 64-B dwordx4 rows, default", 316, n316, short_rows<16, 1, 5, 0>);
+        run("8 pkts/wave, 32-B dword rows, default, +50 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 50>);
+        run("8 pkts/wave, 32-B dword rows, default, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100>);
+        run("8 pkts/wave, 32-B dword rows, default, +150 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 150>);
+        run("8 pkts/wave, 32-B dword rows, default, +200 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 200>);
         run("1 pkt/wave, 256-B dword rows, default", 1084, n1084, short_rows<1, 0, 5, 0>);
         run("8 pkts/wave, 32-B dword rows, default", 1084, n1084, short_rows<8, 0, 34, 0>);
         run("8 pkts/wave, 128-B dwordx4 rows, default", 1084, n1084, short_rows<8, 1, 9, 0>);
