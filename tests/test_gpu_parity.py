@@ -776,10 +776,22 @@ def test_ipv4_checksum_reference_vectors_and_fill(engine):
         assert (int(h[10]) << 8 | int(h[11])) == c and oracle.ipv4_checksum(h) == 0
 
 
-def test_ragged_offsets_beyond_2GiB(engine):
+@pytest.mark.parametrize("variant", [-1, 140])
+def test_ragged_offsets_beyond_2GiB(engine, variant):
     """Offset arrays with entries >= 2^31 and >= 2^32 (v_readlane returns int: widening it must not
-    sign-extend): compute, verify and receive-parse against the oracle."""
+    sign-extend): compute, verify and receive-parse against the oracle.  Variant 140 forces the
+    hybrid dispatch, so the oct kernel sees blocks whose packets lie 2 GiB apart (outside its
+    [-1 GiB, +1 GiB) block window: the per-packet path)."""
     import icrc_amd
+
+    engine.set_variant(variant)
+    try:
+        _offsets_beyond_2gib(engine, icrc_amd)
+    finally:
+        engine.set_variant(-1)
+
+
+def _offsets_beyond_2gib(engine, icrc_amd):
 
     rng = np.random.default_rng(44)
     pkts, _ = [], None
@@ -885,6 +897,43 @@ def test_tiny_batches_every_path(engine, n, variant):
         engine.set_variant(-1)
     assert nerr == 0
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
+
+
+def test_oct_frame_boundaries(engine):
+    """The oct kernel's frame arithmetic at its edges, through the default hybrid dispatch (a batch
+    big enough to split): 1- and 2-frame packets (L = 320 / 324: 10 / 11 rows), 4 frames (1084,
+    1088: 34 rows), the hand-off to the long kernel (1089, 1092), every residue of N mod 8 (the
+    front padding), mixed in blocks and in runs, with trailer write, verify and zeroing."""
+    rng = np.random.default_rng(1088)
+    n = 12000
+    choices = np.array([44, 48, 60, 316, 320, 324, 328, 644, 964, 1080, 1084, 1088, 1092, 1096, 2048, 4156])
+    lens = rng.choice(choices, n).astype(np.uint32)
+    lens[2000:2640] = 1088                      # whole blocks of 4-frame packets
+    lens[3000:3640] = 324                       # whole blocks of 2-frame packets
+    lens[5000:5640] = rng.integers(11, 273, 640) * 4  # every row count 2..34
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    want = oracle_icrcs(buf, off, lens)
+    out, nerr, wrote = run_batch(engine, buf, off, lens, write_trailer=True)
+    assert nerr == 0
+    np.testing.assert_array_equal(out, want)
+    tr = (off + lens.astype(np.uint64) - 4).astype(np.int64)[:, None] + np.arange(4)
+    np.testing.assert_array_equal(wrote[tr].reshape(-1).view("<u4"), want)
+    bad = np.arange(7, n, 97)
+    for i in bad:  # a covered byte: payload, or the IPv4 total length of a 44-byte packet
+        L = int(lens[i])
+        wrote[int(off[i]) + (int(rng.integers(40, L - 4)) if L > 44 else 2)] ^= 0x80
+    d_b, d_o, d_l = dev(wrote), dev(off), dev(lens)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_b.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), n, d_ok.data_ptr(), zero_trailer=True,
+                        stream=stream_handle())
+    torch.cuda.synchronize()
+    ok = d_ok.cpu().numpy()
+    expect = np.ones(n, np.uint8)
+    expect[bad] = 0
+    np.testing.assert_array_equal(ok, expect)
+    assert not d_b.cpu().numpy()[tr].any()
 
 
 def test_split_batches_concurrent_streams(engine):
