@@ -208,3 +208,56 @@ def icrc_quad(img: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0, W
     for n in range(8):
         f ^= _lds(img, fin + n * 4096 + (((acc >> (4 * n)) & 15) << 8))
     return int(~np.uint32(np.bitwise_xor.reduce(f)) & 0xFFFFFFFF)
+
+
+# ---- oct kernel (icrc_oct.hip): eight packets per wavefront in chained 10-row frames -----------
+def icrc_oct_set(img: np.ndarray, pkts, K: int = 10) -> list:
+    """One set of up to eight 4-aligned packets (L % 4 == 0) the way icrc_oct.hip steps it: lane
+    8g + c carries packet g; stream word 8 r + c - z in row r (z = -N mod 8 front padding, so rows
+    are aligned to both ends of the packet); the header masks of rows 0..2 come from a lane table
+    (lane k holds head_mask(k)) read at (kf + 8 j) & 63 — negative k wraps to lanes 57..63, which
+    hold 0; the set runs ceil(Rmax / K) frames of K rows with the accumulator carried; a packet's
+    lanes freeze past its own last row.  Returns the ICRCs."""
+    hm_lane = head_mask(np.arange(64, dtype=np.int64))
+    ng = len(pkts)
+    lanes = np.arange(64, dtype=np.uint32)
+    grp = lanes >> 3
+    col = (lanes & 7).astype(np.int64)
+    N = np.zeros(64, np.int64)
+    R = np.zeros(64, np.int64)
+    words = []
+    for g in range(8):
+        if g < ng:
+            L = pkts[g].size
+            assert L % 4 == 0 and L >= 44
+            n = 1 + (L - 4) // 4
+            words.append(np.frombuffer(pkts[g][: L - 4].tobytes(), "<u4"))
+        else:
+            n = 0
+            words.append(np.zeros(0, np.uint32))
+        N[grp == g] = n
+        R[grp == g] = (n + 7) // 8
+    z = (8 - (N & 7)) & 7
+    kf = col - z                               # stream word of this lane in row 0
+    rmax = int(R.max())
+    acc = np.zeros(64, dtype=np.uint32)
+    for f in range((rmax + K - 1) // K):
+        for j in range(K):
+            r = K * f + j
+            if r >= rmax:
+                break
+            k = kf + 8 * r
+            u = np.zeros(64, np.uint32)
+            for i in range(64):
+                g = int(grp[i])
+                if 1 <= k[i] <= words[g].size:
+                    u[i] = words[g][k[i] - 1]
+            if r < 3:
+                u |= hm_lane[(k & 63).astype(np.int64)]
+            nv = u if r == 0 else (_step_lanes(img, acc, lanes) ^ u)
+            acc = np.where(r < R, nv, acc).astype(np.uint32)
+    fin = KFINAL + lanes * 4
+    fm = np.zeros(64, dtype=np.uint32)
+    for n in range(8):
+        fm ^= _lds(img, fin + n * 4096 + (((acc >> (4 * n)) & 15) << 8))
+    return [int(~np.uint32(np.bitwise_xor.reduce(fm[8 * g: 8 * g + 8])) & 0xFFFFFFFF) for g in range(ng)]

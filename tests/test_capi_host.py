@@ -181,6 +181,22 @@ def test_quad_algorithm_emulation_matches_oracle(seed, W):
         assert kernel_emu.icrc_quad(img, np.frombuffer(pkt, np.uint8), group=G - 1, lead=2, W=W) == want
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_oct_frame_emulation_matches_oracle(seed):
+    """icrc_oct.hip's frame layout on the oct table image: sets of up to eight packets of mixed
+    lengths (1 to 4 frames, every N mod 8), rows aligned to both packet ends, header masks from
+    the lane table with the negative-index wrap, per-lane freeze, against the oracle."""
+    import icrc_amd
+
+    img = icrc_amd.table_image(width=8)
+    rng = np.random.default_rng(300 + seed)
+    sets = [[44, 48, 52, 56, 60, 64, 68, 72], [316] * 8, [320, 324, 316, 1084, 1088, 44, 644, 964],
+            [int(x) * 4 for x in rng.integers(11, 273, 8)], [1084] * 3, [48]]
+    for lens in sets:
+        pk = [rng.integers(0, 256, L, dtype=np.uint8) for L in lens]
+        assert kernel_emu.icrc_oct_set(img, pk) == [oracle.compute_icrc(p) for p in pk], lens
+
+
 def test_header_writer_matches_oracle_packet_writer():
     import icrc_amd
 
