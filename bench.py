@@ -428,6 +428,17 @@ def extra_measurements(eng, stream, args, world):
                                     "trailers_zeroed": zeroed}
     del d_buf, d_out, d_ok
 
+    # C1 at the padded stride (packed 4156 and padded 4224 both measured): every
+    # packet 64-byte aligned, the same 4156 bytes each
+    wp = workloads.write_middle_stream(n, args.pmtu, stride=4224)
+    d_buf = workloads.synthesize(eng, wp, stream=stream)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    _, kms = time_kernel(lambda: eng.compute_strided(d_buf.data_ptr(), 4224, L, n, d_out.data_ptr(), False, stream),
+                         args.steps, args.warmup, world)
+    ex["compute_c1_stride_4224"] = {"kernel_ms": round(kms, 4), "GiB/s": round(n * L / (kms * 1e-3) / GIB, 1),
+                                    "frac_of_peak": frac(kms, n * L)}
+    del d_buf, d_out
+
     # mixed MTU
     wm = workloads.mixed_mtu_stream(4 << 20)
     d_buf = workloads.synthesize(eng, wm, stream=stream)
