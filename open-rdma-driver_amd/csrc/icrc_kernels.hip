@@ -662,7 +662,6 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
             const uint32_t dhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(ohi, f0));
             const uint8_t *dq = p.base + (static_cast<uint64_t>(dlo) | (static_cast<uint64_t>(dhi) << 32));
             uint32_t hv[22];
-            bool hk[22];
 #pragma unroll
             for (uint32_t r = 0; r < 22; ++r) {  // 3 packets per round, 66 >= 64
                 const uint32_t j = 3u * r + g;
@@ -670,24 +669,24 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
                 const uint32_t jl = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lf)));
                 const uint32_t jlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(olo)));
                 const uint32_t jhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ohi)));
-                hk[r] = g < 3u && j < 64u && 4u * w + 8u <= jl;  // jl = 0 for packets not on this path
+                const bool k = g < 3u && j < 64u && 4u * w + 8u <= jl;  // jl = 0 for packets not on this path
                 const uint8_t *q =
-                    hk[r] ? p.base + (static_cast<uint64_t>(jlo) | (static_cast<uint64_t>(jhi) << 32)) + 4u * w : dq;
+                    k ? p.base + (static_cast<uint64_t>(jlo) | (static_cast<uint64_t>(jhi) << 32)) + 4u * w : dq;
                 hv[r] = *reinterpret_cast<const uint32_t *>(q);
             }
 #pragma unroll
             for (uint32_t r = 0; r < 22; ++r) {
                 const uint32_t j = 3u * r + g;
-                if (g < 3u && j < 64u) sh[j * kRxStride + w] = hk[r] ? hv[r] : 0u;
+                if (g < 3u && j < 64u) sh[j * kRxStride + w] = hv[r];
             }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 18; ++k) sh[lane * kRxStride + k] = 0u;
         }
         __builtin_amdgcn_wave_barrier();
         uint32_t h[18];
 #pragma unroll
-        for (uint32_t k = 0; k < 18; ++k) h[k] = sh[lane * kRxStride + k];
+        for (uint32_t k = 0; k < 18; ++k) {  // words not loaded (dummy reads, short packets) read as 0
+            const uint32_t x = sh[lane * kRxStride + k];
+            h[k] = (fast && 4u * k + 8u <= L) ? x : 0u;
+        }
         if (!fast && L >= ICRC_MIN_PACKET) {  // misaligned or L % 4 != 0: byte-wise, this lane only
 #pragma unroll
             for (uint32_t k = 0; k < 18; ++k) {
