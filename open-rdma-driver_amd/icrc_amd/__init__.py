@@ -22,7 +22,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd.so")
+# ICRC_AMD_LIB: another build of the same library (A/B measurements of two builds in one run)
+LIB_PATH = os.environ.get("ICRC_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd.so")
 
 OK = 0
 EINVAL = -22

@@ -30,6 +30,12 @@ def main():
             b.data_ptr(), L, L, w.n, out.data_ptr(), False, s), w.n * L)
         jobs[f"ragged{L}"] = (lambda b=b, o=o, ln=ln, w=w, out=out: eng.compute_batch(
             b.data_ptr(), o.data_ptr(), ln.data_ptr(), w.n, out.data_ptr(), False, 0, s), w.n * L)
+    w = workloads.mixed_mtu_stream(4 << 20)
+    b2 = workloads.synthesize(eng, w, stream=s)
+    o2, ln2 = torch.from_numpy(np.ascontiguousarray(w.off)).cuda(), torch.from_numpy(np.ascontiguousarray(w.lens)).cuda()
+    out2 = torch.zeros(w.n, dtype=torch.int32, device="cuda")
+    jobs["c2"] = (lambda: eng.compute_batch(b2.data_ptr(), o2.data_ptr(), ln2.data_ptr(), w.n, out2.data_ptr(), False, 0, s),
+                  int(w.lens.astype(np.int64).sum()))
     times = {(j, v): [] for j in jobs for v in variants}
     for _ in range(5):
         for v in variants:
