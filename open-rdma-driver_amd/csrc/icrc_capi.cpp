@@ -114,9 +114,10 @@ int grid_for(const icrc_engine *e, uint32_t n);
 // wave runs on the one-packet pipeline alone.  Otherwise: a uniform strided
 // batch runs on the one-packet pipeline (kDefaultVariant) when its packets are long, on the oct
 // kernel (kDefaultRaggedVariant) when short; a ragged batch is split by length (hybrid
-// dispatch): the oct kernel takes L < kSplitLen (and every packet off the fast paths) on the
-// caller's stream, the long-packet kernel the rest on the engine's side stream, forked from and
-// joined back into the caller's stream, so that each fills the other's tail.
+// dispatch): the oct kernel takes L < split (and every packet off the fast paths), the long-packet
+// kernel the rest — by default one launch of the fused hybrid kernel (icrc_oct.hip), whose
+// long-packet workgroups take each CU as the oct ones retire; under a forced hybrid variant (A/B)
+// two kernels on the caller's stream and the engine's side stream, forked and joined by events.
 int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     const int grid = grid_for(e, p.n);
     p.split_len = 0;
@@ -143,6 +144,9 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     }
     p.variant = short_variant;
     p.split_len = split;
+    // Default: both halves in one launch (the fused hybrid kernel).  A forced hybrid variant
+    // (100 + q, 200 + q: A/B) keeps the two-stream fork / join below.
+    if (!hybrid_forced) return icrc::launch_hybrid(mode, p, grid, grid, stream);
     std::lock_guard<std::mutex> g(e->fork_mu);
     HIP_TRY(hipEventRecord(e->fork_ev, static_cast<hipStream_t>(stream)));
     HIP_TRY(hipStreamWaitEvent(e->side, e->fork_ev, 0));

@@ -94,6 +94,9 @@ int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *str
 // Fixed-frame oct kernel (icrc_oct.hip), variant 40: packets of at most oct_max_len() bytes.
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag = 0);
 uint32_t oct_max_len();
+// The hybrid dispatch with the oct kernel as its short-packet half, in one launch (icrc_oct.hip):
+// grid_oct workgroups of the oct kernel, then grid_long of the long-packet kernel.
+int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);
 // The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
 // short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
 inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 6 ? oct_max_len() + 1u : kSplitLen; }

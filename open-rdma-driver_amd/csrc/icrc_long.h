@@ -1,0 +1,536 @@
+// icrc_long.h — the one-packet-per-wave pipeline (C1 and the long half of a ragged batch), shared
+// by icrc_kernels.hip (the batch and long-packet kernels) and icrc_oct.hip (the fused hybrid
+// kernel, whose long-packet workgroups run long_body).  The algorithm and the lane mapping are
+// described at the top of icrc_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "icrc_device.h"
+#include "icrc_internal.h"
+
+namespace icrc {
+namespace {
+// ---- pipelined path -----------------------------------------------------------------------
+// A wave walks its packets q = 0, 1, 2, ... (packet index first + q * tw) in sets of S
+// packets processed together (S independent CRC chains for ILP); the loads of set t + D are
+// issued before set t is processed (a D-deep register ring), so each wave keeps ~D*S packets
+// (~4 KiB each) in flight against the ~3 us loaded HBM latency.
+constexpr int kRows = 17;  // rows held in registers per packet: L <= 4352 (every MTU <= 4096)
+
+struct SlotMeta {
+    uint8_t *pkt;
+    uint32_t L;
+    int R;      // rows (regular packets)
+    int k0;     // stream index of lane 0 in row 0
+    int kind;   // 0 = no packet, 1 = regular (aligned, 44 <= L, R <= kRows), 2 = irregular
+};
+
+// Ragged batches: (offset, len) of 64 consecutive packets of this wave's chunk, one per lane
+// (one coalesced load each), read back with v_readlane at a wave-uniform index.
+struct MetaBlock {
+    uint32_t off_lo, off_hi, len;  // per lane
+    int block;                     // uniform
+};
+
+__device__ __forceinline__ uint64_t meta_off(const MetaBlock &mb, int l) {
+    return static_cast<uint64_t>(readlane_u32(mb.off_lo, l)) | (static_cast<uint64_t>(readlane_u32(mb.off_hi, l)) << 32);
+}
+
+__device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, uint32_t lo, uint32_t hi,
+                                           int block, uint32_t lane) {
+    const uint32_t i = lo + static_cast<uint32_t>(block) * 64u + lane;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (i < hi) {
+        off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
+        len = p.len ? p.len[i] : p.ulen;
+    }
+    mb.off_lo = static_cast<uint32_t>(off);
+    mb.off_hi = static_cast<uint32_t>(off >> 32);
+    mb.len = len;
+    mb.block = block;
+}
+
+// LONG: the long-packet half of a split batch — packets with L < p.split_len belong to the short-
+// packet kernel and leave the slot empty (kind 0: no loads, no result).
+template <bool LONG = false>
+__device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t lo,
+                                          uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
+    m.kind = 0;
+    m.R = 0;
+    m.k0 = 0;
+    m.pkt = p.base;
+    m.L = 0;
+    if (q >= nq) return;
+    uint64_t off;
+    uint32_t L;
+    if (ragged) {
+        const int block = static_cast<int>(q >> 6);
+        if (block != mb.block) meta_fetch(p, mb, lo, lo + nq, block, lane);
+        const int l = static_cast<int>(q & 63u);
+        off = meta_off(mb, l);
+        L = readlane_u32(mb.len, l);
+    } else {
+        off = static_cast<uint64_t>(lo + q) * p.stride;
+        L = p.ulen;
+    }
+    if (LONG && L < p.split_len) return;
+    m.pkt = p.base + off;
+    m.L = L;
+    m.kind = 2;
+    if (L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(m.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+        const int N = 1 + static_cast<int>((L - 4u) >> 2);
+        const int R = (N + 63) >> 6;
+        if (R <= kRows) {
+            m.kind = 1;
+            m.R = R;
+            m.k0 = N - 64 * R;
+        }
+    }
+}
+
+// Loads of one packet's rows; rows past the
+// packet and every row of a non-regular slot read 0 through the descriptor's range check.
+// ABL = mode | (cache policy << 2): mode 0 real, 1 loads only, 2 CRC only; policy = the aux
+// operand of the row loads (0 default, 2 nt: read-once stream).
+constexpr int abl_mode(int abl) { return abl & 3; }
+constexpr int abl_aux(int abl) { return abl >> 2; }
+
+// Verify also loads the packet's stored trailer (all lanes, one dword) as load kRows of the same
+// ring position, so that the comparison needs no load of its own after the CRC (a load issued
+// there is the youngest in flight and its wait drains the ring).
+template <int MODE>
+constexpr int ring_words() { return MODE == kVerify ? kRows + 1 : kRows; }
+
+template <int ABL, int MODE>
+__device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[ring_words<MODE>()]) {
+    if constexpr (abl_mode(ABL) == 2) {
+#pragma unroll
+        for (int j = 0; j < ring_words<MODE>(); ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
+        return;
+    }
+    constexpr int kAux = abl_aux(ABL);
+    // compute reads [0, L-4); verify also the trailer [L-4, L) (rows never reach it)
+    const int nrec = m.kind == 1 ? static_cast<int>(MODE == kVerify ? m.L : m.L - 4u) : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
+    const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
+    // Always the same loads, no branch: hipcc's static vmcnt accounting takes the minimum over
+    // all paths, so a conditional load block anywhere in the ring turns the waits for the
+    // current packet into vmcnt(0) and drains the prefetch of the next one.
+#pragma unroll
+    for (int j = 0; j < kRows; ++j)
+        u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, kAux);
+    if constexpr (MODE == kVerify)
+        u[kRows] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(m.L - 4u), 0, kAux);
+}
+
+// Result of a regular packet of the pipelined path, from registers only: compute -> the ICRC;
+// verify -> OK / MISMATCH against the trailer word loaded with the rows.  TRAILER: the one
+// trailer store of the packet (compute: the ICRC, PacketWriter::write, packet_processor.rs:263;
+// verify: zeros, is_icrc_valid, 350) as a buffer store that every lane issues, lane 0 in range
+// (no branch, so the ring's vmcnt accounting stays exact; an empty slot's descriptor has size 0).
+template <int MODE, bool TRAILER>
+__device__ __forceinline__ uint32_t regular_result(const SlotMeta &m, uint32_t crc, uint32_t stored, uint32_t lane) {
+    if constexpr (TRAILER) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, m.kind == 1 ? static_cast<int>(m.L) : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs,
+                                              static_cast<int>(lane == 0 ? m.L - 4u : 0x80000000u), 0, 0);
+    }
+    if constexpr (MODE == kCompute) return crc;
+    else return stored == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+// ---- receive parse (icrc_rx_parse_device) --------------------------------------------------
+// `hdr` holds packet word w (bytes 4w .. 4w+3, LE, zero past L-4) in lane w for w < 18: the
+// IPv4 + UDP + BTH + up to 32 bytes of extension headers.  Restates to_rdma_message
+// (packet_processor.rs:18-71) on the UDP payload with the ICRC stripped; field getters
+// packet.rs:57-98 (BTH), 173-183 (RETH), 222-232 (AETH), 249-251 (Immediate).  Lane k < 18
+// stores dword k of the 72-byte icrc_rx_desc.
+// Per-lane constants of the descriptor layout, set once per kernel (rx_lane_init): descriptor
+// dword `lane` <- header word src (a big-endian field, byte-swapped), kept when its class is
+// present.   dword: 0 va.lo  1 va.hi  2 sec.lo  3 sec.hi  7 rkey  8 dlen  9 sec rkey  10 sec dlen
+//                   11 imm  12 dqpn  13 psn  14 aeth msn   <- header words 11 10 15 14 12 13 16 17
+//                   14 8 9 10.   Classes: 1 RETH, 2 secondary RETH, 4 Imm, 8 AETH, 16 BTH.
+__device__ __forceinline__ void rx_lane_init(LaneConsts &c, uint32_t lane) {
+    uint32_t src = 0, cls = 0;
+    src = lane == 0u ? 11u : src;
+    src = lane == 1u ? 10u : src;
+    src = lane == 2u ? 15u : src;
+    src = lane == 3u ? 14u : src;
+    src = lane == 7u ? 12u : src;
+    src = lane == 8u ? 13u : src;
+    src = lane == 9u ? 16u : src;
+    src = lane == 10u ? 17u : src;
+    src = lane == 11u ? 14u : src;
+    src = lane == 12u ? 8u : src;
+    src = lane == 13u ? 9u : src;
+    src = lane == 14u ? 10u : src;
+    cls = (lane <= 1u || lane == 7u || lane == 8u) ? 1u : cls;
+    cls = (lane == 2u || lane == 3u || lane == 9u || lane == 10u) ? 2u : cls;
+    cls = lane == 11u ? 4u : cls;
+    cls = lane == 14u ? 8u : cls;
+    cls = (lane == 12u || lane == 13u) ? 16u : cls;
+    c.rx_src4 = src << 2;
+    c.rx_cls = cls;
+    c.rx_mask = (lane >= 12u && lane <= 14u) ? 0xFFFFFFu : 0xFFFFFFFFu;
+}
+
+// `hdr` holds packet word w (bytes 4w .. 4w+3, LE, zero past L-4) in lane w for w < 18: the
+// IPv4 + UDP + BTH + up to 32 bytes of extension headers.  Restates to_rdma_message
+// (packet_processor.rs:18-71) on the UDP payload with the ICRC stripped; field getters
+// packet.rs:57-98 (BTH), 173-183 (RETH), 222-232 (AETH), 249-251 (Immediate).  Lane k < 18
+// stores dword k of the 72-byte icrc_rx_desc.  The packet-wide fields are decoded on the
+// scalar unit (three v_readlane), the per-lane ones take one ds_bpermute + v_perm + a class
+// test, and the six computed dwords are selected into their lanes.
+__device__ __forceinline__ void rx_store(icrc_rx_desc *rx, uint32_t i, uint32_t hdr, uint64_t off, uint32_t L,
+                                         uint32_t icrc_ok, uint32_t lane, const LaneConsts &c) {
+    const uint32_t w7 = readlane_u32(hdr, 7), w9 = readlane_u32(hdr, 9), w10 = readlane_u32(hdr, 10);
+    const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+    // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
+    const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                      : (op == 0x0Cu)                 ? 44u
+                      : (op == 0x11u)                 ? 16u
+                      : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                      : 0u;
+    const uint32_t status = (L < ICRC_MIN_PACKET)   ? ICRC_RX_TRUNCATED
+                          : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
+                          : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
+                          : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
+                                                    : ICRC_RX_OK;
+    const bool ack = hs == 16u;
+    const bool ok = status == ICRC_RX_OK;
+    const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                           (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                           (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+    const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+    const uint64_t poff = off + 28u + hs;
+    // present classes: General metadata has a RETH, Acknowledge an AETH; none on error
+    const uint32_t en = ok ? ((ack ? 8u : 1u) | (hs == 44u ? 2u : 0u) | (hs == 32u ? 4u : 0u) | 16u) : 0u;
+
+    const uint32_t g = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(c.rx_src4), static_cast<int>(hdr)));
+    uint32_t v = __builtin_amdgcn_perm(g, g, 0x00010203u) & c.rx_mask;  // bswap32
+    v = (c.rx_cls & en) ? v : 0u;
+    auto put = [&](uint32_t x, uint32_t l) __attribute__((always_inline)) { v = lane == l ? x : v; };
+    put(ok ? static_cast<uint32_t>(poff) : 0u, 4);
+    put(ok ? static_cast<uint32_t>(poff >> 32) : 0u, 5);
+    put(ok ? L - 32u - hs - pad : 0u, 6);
+    put(ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u, 15);
+    put(ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u, 16);
+    put((icrc_ok & 0xFFu) | (status << 8), 17);
+    if (lane < 18u) reinterpret_cast<uint32_t *>(rx + i)[lane] = v;
+}
+
+// Header words of a packet at any alignment, byte-wise (generic path).
+__device__ __forceinline__ uint32_t rx_header_bytes(const uint8_t *pkt, uint32_t L, uint32_t lane) {
+    uint32_t w = 0;
+    if (lane < 18u && L >= 4u) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t o = 4u * lane + t;
+            w |= (o < L - 4u ? static_cast<uint32_t>(pkt[o]) : 0u) << (8 * t);
+        }
+    }
+    return w;
+}
+
+// PARSE: gather packet words 0..17 into lanes 0..17 from the first two rows as loaded (raw, before
+// the ICRC masks): word w sits in row j, lane w + 1 - k0 - 64 j.
+__device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row1, int k0, uint32_t lane) {
+    const int s0 = static_cast<int>(lane) + 1 - k0;
+    const int s1 = s0 - 64;
+    const uint32_t v0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((s0 & 63) << 2, static_cast<int>(row0)));
+    const uint32_t v1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((s1 & 63) << 2, static_cast<int>(row1)));
+    return (s0 >= 0 && s0 < 64) ? v0 : ((s1 >= 0 && s1 < 64) ? v1 : 0u);
+}
+
+// Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
+// the wave's result buffer.
+// PARSE: 0 off; 1 receive parse (rx_store).
+template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
+__device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                            uint32_t lane, const SlotMeta (&m)[S],
+                                            uint32_t (&u)[S][ring_words<MODE>()], uint32_t q0, ResultBuf &rb,
+                                            uint32_t lo = 0) {
+    int rmax = 0;
+    bool same = true;  // every slot regular with the same row count (the common case)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        if (m[s].kind == 1 && m[s].R > rmax) rmax = m[s].R;
+        same = same && m[s].kind == 1 && m[s].R == m[0].R;
+    }
+    if (rmax > 0) {
+        uint32_t acc[S];
+        uint32_t hdr[S];  // PARSE: packet word w in lane w (w < 18), from rows 0 and 1 as loaded
+        if constexpr (PARSE) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) hdr[s] = rx_gather_header(u[s][0], u[s][1], m[s].k0, lane);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k = m[s].k0 + static_cast<int>(lane);
+            acc[s] = u[s][0] | head_mask(k);
+            u[s][1] |= head_mask(k + 64);
+        }
+        // One straight-line block per row for all S chains (the scheduler interleaves them).
+        if (same && rmax == kRows) {  // full-MTU packets (4 KiB): no per-row guard branches
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                    else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                }
+            }
+        } else if (same) {
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                        else acc[s] = step_m64(lds, acc[s], u[s][j], c);
+                    }
+                }
+            }
+        } else {
+            // a chain past its own last row keeps its value through a select
+#pragma unroll
+            for (int j = 1; j < kRows; ++j) {
+                if (j < rmax) {
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if constexpr (abl_mode(ABL) == 1) {
+                            acc[s] ^= u[s][j];
+                        } else {
+                            const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
+                            acc[s] = (j < m[s].R) ? t : acc[s];
+                        }
+                    }
+                }
+            }
+        }
+        uint32_t fin[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]),
+                                                             MODE == kVerify ? u[s][ring_words<MODE>() - 1] : 0u, lane);
+            if (m[s].kind == 1) {
+                rb_put(rb, q0 + s, r);
+                if constexpr (PARSE)
+                    rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (m[s].kind == 2) {
+            uint32_t hdr_slow = 0;
+            if constexpr (PARSE) hdr_slow = rx_header_bytes(m[s].pkt, m[s].L, lane);  // before any trailer zeroing
+            const uint32_t r = handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane);
+            rb_put(rb, q0 + s, r);
+            if constexpr (PARSE)
+                rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
+        }
+}
+
+// A wave owns the contiguous packet range [lo, lo + nq) and walks it in sets of S packets
+// (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
+// processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
+// ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
+template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false, bool TRAILER = false>
+__device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                              uint32_t lane, uint32_t lo, uint32_t nq) {
+    constexpr int B = D + 1;
+    static_assert(64 % S == 0, "sets must not straddle a 64-packet result block");
+    if (nq == 0) return;
+    const uint32_t nsets = (nq + S - 1) / S;
+    const bool ragged = p.off != nullptr || p.len != nullptr;
+    MetaBlock mb;
+    mb.block = -1;
+    mb.off_lo = mb.off_hi = mb.len = 0;
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    SlotMeta m[B][S];
+    uint32_t u[B][S][ring_words<MODE>()];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (static_cast<uint32_t>(d) < nsets) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                slot_meta<LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
+                slot_load<ABL, MODE>(m[d][s], lane, u[d][s]);
+            }
+        }
+    }
+    for (uint32_t t = 0; t < nsets; t += B) {
+        const bool cont = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            const uint32_t ts = t + b;
+            if (ts >= nsets) return false;
+            const uint32_t tp = ts + D;
+            // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                slot_meta<LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                slot_load<ABL, MODE>(m[bp][s], lane, u[bp][s]);
+            }
+            const uint32_t q0 = ts * S;
+            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, lo);
+            const uint32_t qn = q0 + S;  // next unprocessed
+            if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+            return true;
+        });
+        if (!cont) return;
+    }
+}
+
+// ---- long packets of a ragged batch (hybrid dispatch) ------------------------------------------
+// The one-packet pipeline (S = 1, D-deep prefetch) over only the packets with L >= p.split_len;
+// the quad kernel (icrc_quad.hip) takes the shorter ones, whose per-packet costs it divides by
+// four.  Long packets stay here because one contiguous 256-byte row per wave instruction
+// streams from HBM at ~6.2 TB/s, while four packets per instruction stop at ~4.5 TB/s
+// (profiles/r01_membench.json, patterns D and E).  The walk skips short packets with the
+// ballot of each 64-packet meta block; results are kept per block and stored 64 at a time.
+// Packets in flight ahead of the one being stepped (3 measured the same on C2: the long half's
+// tail is the CUs freeing up from the short-packet kernel, not the walk's latency).
+constexpr int kLongWalkDepth = 1;
+template <int MODE, int D, int ABL, bool TRAILER>
+__device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                                   uint32_t lane, uint32_t lo, uint32_t nq) {
+    constexpr int B = D + 1;
+    if (nq == 0) return;
+    MetaBlock mb;
+    mb.block = -1;
+    mb.off_lo = mb.off_hi = mb.len = 0;
+    uint64_t lmask = 0;  // long packets of mb
+    uint32_t qn = 0;     // next candidate (load side)
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    int rb_block = -1;
+    SlotMeta m[B][1];
+    uint32_t qs[B];
+    uint32_t u[B][1][ring_words<MODE>()];
+    int inflight = 0;
+
+    auto next = [&](SlotMeta &sm, uint32_t &q) __attribute__((always_inline)) {
+        sm.kind = 0;
+        sm.R = 0;
+        sm.k0 = 0;
+        sm.pkt = p.base;
+        sm.L = 0;
+        q = 0xFFFFFFFFu;
+        while (qn < nq) {
+            const int blk = static_cast<int>(qn >> 6);
+            if (blk != mb.block) {
+                meta_fetch(p, mb, lo, lo + nq, blk, lane);
+                lmask = __ballot(static_cast<uint32_t>(blk) * 64u + lane < nq && mb.len >= p.split_len);
+            }
+            const uint64_t mask = lmask & (~0ull << (qn & 63u));
+            if (mask == 0) {
+                qn = static_cast<uint32_t>(blk + 1) * 64u;
+                continue;
+            }
+            const int l = __builtin_ctzll(mask);
+            q = static_cast<uint32_t>(blk) * 64u + static_cast<uint32_t>(l);
+            qn = q + 1u;
+            const uint64_t off = meta_off(mb, l);
+            const uint32_t L = readlane_u32(mb.len, l);
+            sm.pkt = p.base + off;
+            sm.L = L;
+            sm.kind = 2;
+            if (((reinterpret_cast<uintptr_t>(sm.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+                const int N = 1 + static_cast<int>((L - 4u) >> 2);
+                const int R = (N + 63) >> 6;
+                if (R <= kRows) {
+                    sm.kind = 1;
+                    sm.R = R;
+                    sm.k0 = N - 64 * R;
+                }
+            }
+            return;
+        }
+    };
+
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        next(m[d][0], qs[d]);
+        slot_load<ABL, MODE>(m[d][0], lane, u[d][0]);
+        if (m[d][0].kind) inflight += 1;
+    }
+    for (;;) {
+        static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + D) % B;
+            next(m[bp][0], qs[bp]);
+            slot_load<ABL, MODE>(m[bp][0], lane, u[bp][0]);
+            if (m[bp][0].kind) inflight += 1;
+            if (m[b][0].kind) {
+                const int blk = static_cast<int>(qs[b] >> 6);
+                if (blk != rb_block) {
+                    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+                    rb_block = blk;
+                }
+                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, lo);
+                inflight -= 1;
+            }
+            return true;
+        });
+        if (qn >= nq && inflight == 0) break;
+    }
+    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+}
+
+// Default (COMPACT = false): per wave, the C1 pipeline (S = 2 chains, D = 1) over the wave's whole
+// chunk with short packets left as empty slots when long packets are dense — on an all-long ragged
+// batch it runs at the strided rate (1 Mi x 4156 B: 0.75 ms split vs 0.80-0.87 with the walker) —
+// and the compacting S = 1 walker above when they are sparse (on a mixed-MTU batch the dense walk
+// costs 1.32 ms against 0.49).  COMPACT = true: the walker always (A/B: variant 200 + q).
+// The long-packet kernel's work for workgroup `bid` of `nblk` (its own kernel, or the long-packet
+// workgroups of the fused hybrid kernel, icrc_oct.hip).
+template <int MODE, bool COMPACT, bool TRAILER>
+__device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
+        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
+    c.fin = kFinalBase + lane * 4u;
+    const uint32_t tw = nblk * kWavesPerGroup;
+    const uint32_t gw = bid * kWavesPerGroup + wave;
+    const uint32_t chunk = wave_chunk(p.n, tw);
+    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    if (lo64 >= p.n) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    if constexpr (COMPACT) {
+        run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+    } else {
+        // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
+        // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
+        // (a mixed-MTU batch: ~1.5 % long) -> the compacting walker, which visits long packets only.
+        const uint32_t L0 = lane < nq ? (p.len ? p.len[lo + lane] : p.ulen) : 0u;
+        const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
+        const uint32_t nb = nq < 64u ? nq : 64u;
+        if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
+            run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
+        else
+            run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+    }
+}
+
+}  // namespace
+}  // namespace icrc

@@ -38,6 +38,7 @@
 
 #include "icrc_device.h"
 #include "icrc_internal.h"
+#include "icrc_long.h"
 
 namespace icrc {
 namespace {
@@ -542,17 +543,18 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     }
 }
 
+// The oct kernel's work for workgroup `bid` of `nblk` (its own kernel, or the short-packet
+// workgroups of the fused hybrid kernel below).
 template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
-__global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams p) {
-    __shared__ uint4 lds4[kLdsBytes / 16];
-    const uint32_t tw = gridDim.x * kWavesPerGroup;
+__device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
+    const uint32_t tw = nblk * kWavesPerGroup;
     // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
     uint32_t chunk = (p.n + tw - 1) / tw;
     chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 7u) & ~7u;
     if (RAGGED && p.split_len != 0 && p.len != nullptr) {
         // Split batch: a workgroup whose packets are all the long-packet kernel's exits before
         // its 160 KiB table load.
-        const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk;
+        const uint64_t g0 = static_cast<uint64_t>(bid) * kWavesPerGroup * chunk;
         const uint64_t g1 = g0 + static_cast<uint64_t>(kWavesPerGroup) * chunk;
         const uint64_t end = g1 < p.n ? g1 : p.n;
         bool any_short = false;
@@ -577,12 +579,30 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams 
     LaneConsts c;
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
-    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t gw = bid * kWavesPerGroup + wave;
     const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
     run_oct<MODE, RAGGED, TRAILER, DIAG>(p, lds, c, lane, lo, nq);
+}
+
+template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    oct_body<MODE, RAGGED, TRAILER, DIAG>(p, lds4, blockIdx.x, gridDim.x);
+}
+
+// The hybrid dispatch in ONE launch: workgroups [0, g_oct) are the oct kernel's (L < split_len),
+// the rest the long-packet kernel's (L >= split_len).  Each loads its own table image.  Workgroups
+// are dispatched in index order, so the long-packet ones take each CU as its oct workgroup
+// retires — the overlap the two-stream fork / join gave, without its cross-queue wait (~19 us per
+// call, profiles/r02_hybrid_fused.jsonl) or the second launch.
+template <int MODE, bool TRAILER, bool COMPACT>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_kernel(BatchParams p, uint32_t g_oct) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, 0>(p, lds4, blockIdx.x, g_oct);
+    else long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
 }
 
 }  // namespace
@@ -623,6 +643,28 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
 #undef ICRC_OM
 #undef ICRC_OD
 #undef ICRC_O
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 g(static_cast<uint32_t>(grid_oct + grid_long));
+    const uint32_t go = static_cast<uint32_t>(grid_oct);
+#define ICRC_H(M, T, C) hipLaunchKernelGGL((icrc_hybrid_kernel<M, T, C>), g, dim3(kThreadsPerGroup), 0, s, p, go)
+#define ICRC_HM(M)                                    \
+    do {                                              \
+        if (p.long_variant == 1) {                    \
+            if (p.trailer) ICRC_H(M, true, true);     \
+            else ICRC_H(M, false, true);              \
+        } else {                                      \
+            if (p.trailer) ICRC_H(M, true, false);    \
+            else ICRC_H(M, false, false);             \
+        }                                             \
+    } while (0)
+    if (mode == kCompute) ICRC_HM(kCompute);
+    else ICRC_HM(kVerify);
+#undef ICRC_HM
+#undef ICRC_H
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
