@@ -498,6 +498,21 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
 // workgroups of the fused hybrid kernel, icrc_oct.hip).
 template <int MODE, bool COMPACT, bool TRAILER>
 __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
+    if (p.split_len != 0 && p.len != nullptr) {
+        // A workgroup whose packets are all the oct kernel's exits before its 160 KiB table load.
+        const uint64_t per = static_cast<uint64_t>(kWavesPerGroup) * wave_chunk(p.n, nblk * kWavesPerGroup);
+        const uint64_t g0 = static_cast<uint64_t>(bid) * per, g1 = g0 + per < p.n ? g0 + per : p.n;
+        bool any_long = false;
+        for (uint64_t i = g0 + threadIdx.x; i < g1; i += kThreadsPerGroup) any_long |= p.len[i] >= p.split_len;
+        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(lds4);
+        if (threadIdx.x == 0) *flag = 0u;
+        __syncthreads();
+        if (any_long) *flag = 1u;
+        __syncthreads();
+        const bool go = *flag != 0u;
+        __syncthreads();  // every wave has read the flag before the table load overwrites it
+        if (!go) return;
+    }
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
         for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
