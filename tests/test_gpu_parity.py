@@ -1089,3 +1089,43 @@ def test_packetize_read_requests_and_oversize(engine):
     np.testing.assert_array_equal(gl, wl)
     np.testing.assert_array_equal(gi, wi)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("variant", [-1, 140])
+def test_hybrid_segregated_halves(engine, variant):
+    """The one-launch hybrid kernel (default) and the two-kernel fork / join (140) on a ragged
+    batch whose first half is all 4156-byte packets and second half all 316-byte ones: the oct
+    workgroups over the first half and the long-packet workgroups over the second both exit before
+    their table loads.  Compute with write_trailer, then verify with zero_trailer, against the
+    oracle; one flipped bit in each half must read as a mismatch."""
+    n_long, n_short = 8192, 8192
+    bl, _, ll = oracle.synth_middle_stream(n_long, pmtu=4096)
+    bs, _, ls = oracle.synth_middle_stream(n_short, pmtu=256, payload_key=0xBEEF)
+    buf = np.concatenate([bl, bs])
+    lens = np.concatenate([ll, ls]).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    assert int(off[-1]) + int(lens[-1]) == buf.size
+    want = oracle_icrcs(buf, off, lens)
+    engine.set_variant(variant)
+    try:
+        out, nerr, after = run_batch(engine, buf, off, lens, write_trailer=True)
+        assert nerr == 0
+        assert np.array_equal(out, want)
+        tr = np.stack([after[int(o) + int(L) - 4: int(o) + int(L)] for o, L in zip(off, lens)])
+        assert np.array_equal(tr.view("<u4").ravel(), want)
+        flips = [5, n_long + 7]
+        for i in flips:
+            after[int(off[i]) + 100] ^= 0x10
+        d_buf, d_off, d_len = dev(after), dev(off), dev(lens)
+        d_ok = torch.zeros(len(lens), dtype=torch.uint8, device="cuda")
+        engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(lens), d_ok.data_ptr(),
+                            zero_trailer=True, stream=stream_handle())
+        torch.cuda.synchronize()
+        ok = d_ok.cpu().numpy()
+        expect = np.ones(len(lens), np.uint8)
+        expect[flips] = 0
+        assert np.array_equal(ok, expect)
+        zb = d_buf.cpu().numpy()
+        assert all(not zb[int(o) + int(L) - 4: int(o) + int(L)].any() for o, L in zip(off, lens))
+    finally:
+        engine.set_variant(-1)
