@@ -494,6 +494,29 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
 // batch it runs at the strided rate (1 Mi x 4156 B: 0.75 ms split vs 0.80-0.87 with the walker) —
 // and the compacting S = 1 walker above when they are sparse (on a mixed-MTU batch the dense walk
 // costs 1.32 ms against 0.49).  COMPACT = true: the walker always (A/B: variant 200 + q).
+// Split batches (hybrid dispatch): whether any packet in [g0, end) is short (SHORT: L < split_len)
+// or long (!SHORT).  Every thread of the workgroup calls it; the waves scan 1024-packet strides
+// and stop as soon as one of them has found such a packet (a flag in LDS word 0, which the caller
+// overwrites with its tables only after the last barrier here).
+template <bool SHORT>
+__device__ __forceinline__ bool wg_any_split(const BatchParams &p, uint4 *lds4, uint64_t g0, uint64_t end) {
+    volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(lds4);
+    if (threadIdx.x == 0) *flag = 0u;
+    __syncthreads();
+    for (uint64_t b = g0; b < end; b += kThreadsPerGroup) {
+        const uint64_t i = b + threadIdx.x;
+        if (__ballot(i < end && (p.len[i] < p.split_len) == SHORT) != 0ull) {
+            *flag = 1u;
+            break;
+        }
+        if (__builtin_amdgcn_readfirstlane(static_cast<int>(*flag)) != 0) break;
+    }
+    __syncthreads();
+    const bool go = *flag != 0u;
+    __syncthreads();  // every wave has read the flag before the caller's table load overwrites it
+    return go;
+}
+
 // The long-packet kernel's work for workgroup `bid` of `nblk` (its own kernel, or the long-packet
 // workgroups of the fused hybrid kernel, icrc_oct.hip).
 template <int MODE, bool COMPACT, bool TRAILER>
@@ -502,16 +525,7 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         // A workgroup whose packets are all the oct kernel's exits before its 160 KiB table load.
         const uint64_t per = static_cast<uint64_t>(kWavesPerGroup) * wave_chunk(p.n, nblk * kWavesPerGroup);
         const uint64_t g0 = static_cast<uint64_t>(bid) * per, g1 = g0 + per < p.n ? g0 + per : p.n;
-        bool any_long = false;
-        for (uint64_t i = g0 + threadIdx.x; i < g1; i += kThreadsPerGroup) any_long |= p.len[i] >= p.split_len;
-        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(lds4);
-        if (threadIdx.x == 0) *flag = 0u;
-        __syncthreads();
-        if (any_long) *flag = 1u;
-        __syncthreads();
-        const bool go = *flag != 0u;
-        __syncthreads();  // every wave has read the flag before the table load overwrites it
-        if (!go) return;
+        if (!wg_any_split<false>(p, lds4, g0, g1)) return;
     }
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(p.table);

@@ -557,16 +557,7 @@ __device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint
         const uint64_t g0 = static_cast<uint64_t>(bid) * kWavesPerGroup * chunk;
         const uint64_t g1 = g0 + static_cast<uint64_t>(kWavesPerGroup) * chunk;
         const uint64_t end = g1 < p.n ? g1 : p.n;
-        bool any_short = false;
-        for (uint64_t i = g0 + threadIdx.x; i < end; i += kThreadsPerGroup) any_short |= p.len[i] < p.split_len;
-        volatile uint32_t *flag = reinterpret_cast<volatile uint32_t *>(lds4);
-        if (threadIdx.x == 0) *flag = 0u;
-        __syncthreads();
-        if (any_short) *flag = 1u;
-        __syncthreads();
-        const bool go = *flag != 0u;
-        __syncthreads();  // every wave has read the flag before the table load overwrites it
-        if (!go) return;
+        if (!wg_any_split<true>(p, lds4, g0, end)) return;
     }
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(p.table_oct);
