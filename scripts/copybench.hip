@@ -1,0 +1,209 @@
+// copybench.hip — the ceiling of the send packetizer's copy shape (measurement tool, not product
+// code).  786 432 payloads of 4096 B (contiguous) become 4156-B wire packets (payload at packet
+// offset 56, packets 4156 B apart, so the payload lands 4-B aligned).  Forms:
+//   rows_dword<W>   256-B dword rows (the packetizer's shape), W waves per CU
+//   rows_x4<W>      1-KiB dwordx4 rows (16 B per lane), W waves per CU
+//   flat_x4         contiguous float4 grid-stride copy of the same byte count
+//   hipMemcpy       device-to-device copy of the same byte count
+// GB/s counts read + write bytes.  Output: one JSON line per form.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                             \
+        }                                                                        \
+    } while (0)
+
+constexpr uint32_t kPay = 4096, kWire = 4156, kN = 786432, kHdr = 56;
+
+// one wave per packet, contiguous chunks, the next packet's rows loaded while the current one is
+// stored (a two-slot register ring)
+template <int POLICY_ST, bool IL = false>
+__global__ __launch_bounds__(1024) void rows_dword(const uint8_t *src, uint8_t *dst, uint32_t waves) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // IL: packet q of the wave is gw + q * waves (the grid sweeps memory together); else the
+    // wave owns the contiguous range [gw * chunk, ...)
+    const uint32_t chunk = (kN + waves - 1) / waves;
+    const uint32_t lo = IL ? 0u : gw * chunk;
+    if (gw * chunk >= kN) return;
+    const uint32_t nq = IL ? (kN - gw + waves - 1) / waves : (kN - lo < chunk ? kN - lo : chunk);
+    auto pkt = [&](uint32_t q) -> size_t { return IL ? (size_t)gw + (size_t)q * waves : (size_t)(lo + q); };
+    constexpr int R = 16;
+    uint32_t ua[R], ub[R];
+    auto load = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + pkt(q) * kPay), 0, (int)kPay, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * lane + 256u * j), 0, 0);
+    };
+    auto store = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + pkt(q) * kWire), 0, (int)kWire, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            __builtin_amdgcn_raw_buffer_store_b32(u[j], rs, (int)(kHdr + 4u * lane + 256u * j), 0, POLICY_ST);
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        store(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        store(q + 1, ub);
+    }
+}
+
+template <int POLICY_ST, bool IL = false>
+__global__ __launch_bounds__(1024) void rows_x4(const uint8_t *src, uint8_t *dst, uint32_t waves) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // IL: packet q of the wave is gw + q * waves (the grid sweeps memory together); else the
+    // wave owns the contiguous range [gw * chunk, ...)
+    const uint32_t chunk = (kN + waves - 1) / waves;
+    const uint32_t lo = IL ? 0u : gw * chunk;
+    if (gw * chunk >= kN) return;
+    const uint32_t nq = IL ? (kN - gw + waves - 1) / waves : (kN - lo < chunk ? kN - lo : chunk);
+    auto pkt = [&](uint32_t q) -> size_t { return IL ? (size_t)gw + (size_t)q * waves : (size_t)(lo + q); };
+    constexpr int R = 4;
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    v4 ua[R], ub[R];
+    auto load = [&](uint32_t q, v4 (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + pkt(q) * kPay), 0, (int)kPay, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * lane + 1024u * j), 0, 0);
+    };
+    auto store = [&](uint32_t q, v4 (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + pkt(q) * kWire), 0, (int)kWire, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(u[j], rs, (int)(kHdr + 16u * lane + 1024u * j), 0, POLICY_ST);
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        store(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        store(q + 1, ub);
+    }
+}
+
+// the C1 read shape alone: 1 Mi x 4156-B packets, 17 dword rows per packet, nt loads
+template <bool IL>
+__global__ __launch_bounds__(1024) void read_rows(const uint8_t *src, uint32_t *out, uint32_t waves, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t chunk = (n + waves - 1) / waves;
+    if (gw * chunk >= n) return;
+    const uint32_t nq = IL ? (n - gw + waves - 1) / waves : (n - gw * chunk < chunk ? n - gw * chunk : chunk);
+    auto pkt = [&](uint32_t q) -> size_t { return IL ? (size_t)gw + (size_t)q * waves : (size_t)gw * chunk + q; };
+    constexpr int R = 17;
+    uint32_t ua[R], ub[R], acc = 0;
+    auto load = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + pkt(q) * 4156u), 0, 4152, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * lane + 256u * j) - 200, 0, 2);
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc ^= ua[j];
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc ^= ub[j];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void flat_x4(const uint4 *s, uint4 *d, size_t n16) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) d[i] = s[i];
+}
+
+template <class F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main() {
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    uint8_t *src, *dst;
+    const size_t src_bytes = (size_t)1048576 * 4156 + 4096;  // >= kN * kPay; the C1 read shape reads 1 Mi x 4156 B
+    CK(hipMalloc(&src, src_bytes));
+    CK(hipMalloc(&dst, (size_t)kN * kWire + 4096));
+    CK(hipMemset(src, 0x5a, src_bytes));
+    CK(hipMemset(dst, 0, (size_t)kN * kWire));
+    const int reps = 10;
+    const double wire_bytes = (double)kN * (kPay + kPay);  // payload read + payload written
+    auto report = [&](const char *name, float ms) {
+        printf("{\"form\": \"%s\", \"ms\": %.4f, \"GB/s (read+write)\": %.1f}\n", name, ms, wire_bytes / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    };
+    for (int rep = 0; rep < 2; ++rep) {
+        {
+            // read shape (C1): 1 Mi x 4156 B of src
+            const uint32_t n = 1048576u;
+            const double rb = (double)n * 4152;
+            uint32_t *o = (uint32_t *)dst;  // written only if the XOR hits a magic value
+            float ms = time_it([&] { read_rows<false><<<cus, 1024>>>(src, o, cus * 16, n); }, reps);
+            printf("{\"form\": \"read C1 shape, contiguous chunks\", \"ms\": %.4f, \"GB/s (read)\": %.1f}\n", ms, rb / (ms * 1e-3) / 1e9);
+            ms = time_it([&] { read_rows<true><<<cus, 1024>>>(src, o, cus * 16, n); }, reps);
+            printf("{\"form\": \"read C1 shape, interleaved packets\", \"ms\": %.4f, \"GB/s (read)\": %.1f}\n", ms, rb / (ms * 1e-3) / 1e9);
+        }
+        for (int w : {16, 32}) {
+            const uint32_t waves = cus * w;
+            const int grid = cus * (w / 16);
+            char nm[96];
+            snprintf(nm, sizeof nm, "rows_dword %d waves/CU, interleaved packets", w);
+            report(nm, time_it([&] { rows_dword<0, true><<<grid, 1024>>>(src, dst, waves); }, reps));
+            snprintf(nm, sizeof nm, "rows_x4 %d waves/CU, interleaved packets", w);
+            report(nm, time_it([&] { rows_x4<0, true><<<grid, 1024>>>(src, dst, waves); }, reps));
+            snprintf(nm, sizeof nm, "rows_x4 %d waves/CU, interleaved packets, nt stores", w);
+            report(nm, time_it([&] { rows_x4<2, true><<<grid, 1024>>>(src, dst, waves); }, reps));
+        }
+        for (int w : {16, 32}) {
+            const uint32_t waves = cus * w;
+            const int grid = cus * (w / 16);
+            char nm[96];
+            snprintf(nm, sizeof nm, "rows_dword %d waves/CU", w);
+            report(nm, time_it([&] { rows_dword<0><<<grid, 1024>>>(src, dst, waves); }, reps));
+            snprintf(nm, sizeof nm, "rows_dword %d waves/CU, nt stores", w);
+            report(nm, time_it([&] { rows_dword<2><<<grid, 1024>>>(src, dst, waves); }, reps));
+            snprintf(nm, sizeof nm, "rows_x4 %d waves/CU", w);
+            report(nm, time_it([&] { rows_x4<0><<<grid, 1024>>>(src, dst, waves); }, reps));
+            snprintf(nm, sizeof nm, "rows_x4 %d waves/CU, nt stores", w);
+            report(nm, time_it([&] { rows_x4<2><<<grid, 1024>>>(src, dst, waves); }, reps));
+        }
+        const size_t n16 = (size_t)kN * kPay / 16;
+        for (int w : {8, 16, 32}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "flat_x4 contiguous %d waves/CU", w);
+            report(nm, time_it([&] { flat_x4<<<cus * w / 4, 256>>>((const uint4 *)src, (uint4 *)dst, n16); }, reps));
+        }
+        report("hipMemcpyDtoD contiguous",
+               time_it([&] { CK(hipMemcpyAsync(dst, src, (size_t)kN * kPay, hipMemcpyDeviceToDevice, 0)); }, reps));
+    }
+    CK(hipFree(src));
+    CK(hipFree(dst));
+    return 0;
+}
