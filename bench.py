@@ -201,7 +201,7 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     wall, kms = time_kernel(step, args.steps, args.warmup, world)
     bytes_per_step = n * L
     # SURVEY 8(d) secondary denominator, same box and batch, after the timed region: the
-    # kernel's loads-only build (variant 15: the same row loads, ring and waits, no CRC)
+    # kernel's loads-only build (variant 19: the same row loads, ring and waits, no CRC)
     eng.set_variant(LOADS_ONLY_VARIANT)
     _, loads_ms = time_kernel(step, min(args.steps, 20), 3, world)
     eng.set_variant(-1)
@@ -256,7 +256,7 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
                 "GB/s": round(bytes_per_step / (loads_ms * 1e-3) / 1e9, 1),
                 "kernel_ms": round(loads_ms, 4),
                 "frac": round(loads_ms / kms, 4),
-                "source": "the same kernel's loads-only build (variant 15: same row loads and ring, no "
+                "source": "the same kernel's loads-only build (variant 19: same row loads and ring, no "
                           "CRC) on the same batch, timed after the K steps; frac = achieved / achievable",
             },
         },
@@ -308,7 +308,7 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
 
 
 PMC_TRAFFIC_FILE = "r02_pmc_traffic.json"
-LOADS_ONLY_VARIANT = 15  # icrc_batch_kernel's ABL loads-only build (csrc/icrc_kernels.hip)
+LOADS_ONLY_VARIANT = 19  # icrc_batch_kernel<.., S = 2, D = 1, loads only>: the default ring without the CRC
 
 
 def pmc_traffic(n: int, L: int):
