@@ -247,6 +247,17 @@ __device__ __forceinline__ uint32_t rx_gather_header(uint32_t row0, uint32_t row
     return (s0 >= 0 && s0 < 64) ? v0 : ((s1 >= 0 && s1 < 64) ? v1 : 0u);
 }
 
+// The header masks of rows 0 and 1 for the last k0 seen (k0 is wave-uniform and, in a strided
+// batch, the same for every packet: the masks are computed once per wave instead of per packet).
+struct HeadMasks {
+    int k0;
+    uint32_t m0, m1;
+};
+__device__ __forceinline__ void head_masks_init(HeadMasks &hm) {
+    hm.k0 = INT32_MIN;
+    hm.m0 = hm.m1 = 0;
+}
+
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
 // the wave's result buffer.
 // PARSE: 0 off; 1 receive parse (rx_store).
@@ -254,7 +265,7 @@ template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
                                             uint32_t lane, const SlotMeta (&m)[S],
                                             uint32_t (&u)[S][ring_words<MODE>()], uint32_t q0, ResultBuf &rb,
-                                            uint32_t lo = 0) {
+                                            HeadMasks &hm, uint32_t lo = 0) {
     int rmax = 0;
     bool same = true;  // every slot regular with the same row count (the common case)
 #pragma unroll
@@ -271,9 +282,13 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const int k = m[s].k0 + static_cast<int>(lane);
-            acc[s] = u[s][0] | head_mask(k);
-            u[s][1] |= head_mask(k + 64);
+            if (m[s].kind == 1 && m[s].k0 != hm.k0) {  // uniform branch, no memory access
+                hm.k0 = m[s].k0;
+                hm.m0 = head_mask(hm.k0 + static_cast<int>(lane));
+                hm.m1 = head_mask(hm.k0 + static_cast<int>(lane) + 64);
+            }
+            acc[s] = u[s][0] | hm.m0;  // slots of kind != 1 are never stored
+            u[s][1] |= hm.m1;
         }
         // One straight-line block per row for all S chains (the scheduler interleaves them).
         if (same && rmax == kRows) {  // full-MTU packets (4 KiB): no per-row guard branches
@@ -357,6 +372,8 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     ResultBuf rb;
     rb.v = 0;
     rb.valid = 0;
+    HeadMasks hm;
+    head_masks_init(hm);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
 #pragma unroll
@@ -383,7 +400,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
                 slot_load<ABL, MODE>(m[bp][s], lane, u[bp][s]);
             }
             const uint32_t q0 = ts * S;
-            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, lo);
+            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, lo);
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             return true;
@@ -416,6 +433,8 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     rb.v = 0;
     rb.valid = 0;
     int rb_block = -1;
+    HeadMasks hm;
+    head_masks_init(hm);
     SlotMeta m[B][1];
     uint32_t qs[B];
     uint32_t u[B][1][ring_words<MODE>()];
@@ -479,7 +498,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
                     if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
                     rb_block = blk;
                 }
-                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, lo);
+                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, lo);
                 inflight -= 1;
             }
             return true;
