@@ -585,7 +585,9 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
             constexpr int b = decltype(bc)::value;
             constexpr int bp = (b + D) % B;
             if (!g[b].fast) return false;  // the ring ran dry: every later slot is empty too
+            __builtin_amdgcn_s_setprio(3);  // the payload loads leave ahead of other waves' stores / row steps
             fill(g[bp], hv[bp], u[bp]);
+            __builtin_amdgcn_s_setprio(0);
             process(g[b], hv[b], u[b]);
             return true;
         });
@@ -798,7 +800,8 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 
 // Variants: 0 one packet per wave, no pipelining; 13 one chain per wave (S = 1, D = 1); 16 two
 // chains (S = 2, D = 1, the default for long packets); 15 / 18 diagnostics of the S = 1, D = 2
-// shape (loads only / CRC only: wrong results by design); 19 loads only of variant 16's ring; 20, 24-26, 31, 32, 35: the quad /
+// shape (loads only / CRC only: wrong results by design); 19 loads only of variant 16's ring; 17
+// variant 16 without the raised wave priority around its load bursts; 20, 24-26, 31, 32, 35: the quad /
 // chunked oct kernels (icrc_quad.hip); 40: the fixed-frame oct kernel (icrc_oct.hip, default
 // for short packets).
 template <int MODE>
@@ -809,6 +812,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2), false); break;  // diagnostic: loads only, nt
     case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2), false); break;  // diagnostic: CRC only (same shape as 15)
     case 19: ICRC_LAUNCH(2, 1, 1 | (2 << 2), false); break;  // diagnostic: loads only of the default (16) ring
+    case 17: ICRC_LAUNCH_T(2, 1, (2 << 2) | kAblNoPrio); break;  // 16 without the raised priority (A/B)
     case 20:
     case 24:
     case 25:

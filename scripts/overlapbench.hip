@@ -71,7 +71,9 @@ __device__ __forceinline__ void load_rows(const Args &a, uint32_t pk, bool live,
 // ranges; 1 sets handed out by per-XCD tickets; 2 by per-workgroup tickets.  A ticket is a buffer
 // atomic (lane 0 in range, the others out of range: no branch) issued BEFORE the loads of the set
 // in flight and read one iteration later, so waiting for it never waits for those loads.
-template <int MODE, int S, bool T64, int DYN>
+// OPT: 0 plain; 1 s_setprio(3) around each set's load burst; 2 the next set's row loads issued
+// one row per row step of the current set (pinned by sched_barrier)
+template <int MODE, int S, bool T64, int DYN, int OPT = 0>
 __device__ __forceinline__ void body(const Args &a, const char *lds) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -113,21 +115,62 @@ __device__ __forceinline__ void body(const Args &a, const char *lds) {
 #pragma unroll
         for (int s = 0; s < S; ++s) tot ^= acc[s] * (set_pk(st, s) | 1u);
     };
+    // OPT 2: step row j of the current set, then load row j of the next one
+    auto process_il = [&](uint32_t (&u)[S][kR], uint32_t st, uint32_t (&v)[S][kR], uint32_t nst) {
+        __amdgpu_buffer_rsrc_t rs[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            rs[s] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.base) + (size_t)set_pk(nst, s) * kL, 0,
+                                                      live(nst) ? (int)(kL - 4) : 0, 0x00020000);
+        const uint32_t vb = 4u * (lane - 50u);
+        uint32_t acc[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            acc[s] = u[s][0];
+            v[s][0] = __builtin_amdgcn_raw_buffer_load_b32(rs[s], (int)vb, 0, 2);
+        }
+#pragma unroll
+        for (int j = 1; j < (int)kR; ++j) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) acc[s] = step<T64>(lds, acc[s], u[s][j], pc);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < S; ++s) v[s][j] = __builtin_amdgcn_raw_buffer_load_b32(rs[s], (int)(vb + 256u * j), 0, 2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) tot ^= acc[s] * (set_pk(st, s) | 1u);
+    };
+    if constexpr (OPT == 2) {
+        for (uint32_t it = 0;; it += 2) {
+            if (!live(cur)) break;
+            process_il(ua, cur, ub, it + 1);
+            cur = it + 1;
+            if (!live(cur)) break;
+            process_il(ub, cur, ua, it + 2);
+            cur = it + 2;
+        }
+    } else {
     for (uint32_t it = 0;; it += 2) {
         uint32_t nb = DYN ? take(nraw) : it + 1;
         if (DYN) nraw = req();
+        if (OPT == 1) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
         for (int s = 0; s < S; ++s) load_rows(a, set_pk(nb, s), live(nb), lane, ub[s]);
+        if (OPT == 1) __builtin_amdgcn_s_setprio(0);
         if (!live(cur)) break;
         process(ua, cur);
         cur = nb;
         nb = DYN ? take(nraw) : it + 2;
         if (DYN) nraw = req();
+        if (OPT == 1) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
         for (int s = 0; s < S; ++s) load_rows(a, set_pk(nb, s), live(nb), lane, ua[s]);
+        if (OPT == 1) __builtin_amdgcn_s_setprio(0);
         if (!live(cur)) break;
         process(ub, cur);
         cur = nb;
+    }
     }
     a.out[gw * 64u + lane] = tot;
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -137,7 +180,7 @@ __device__ __forceinline__ void body(const Args &a, const char *lds) {
     }
 }
 
-template <int MODE, int S, bool T64, int DYN>
+template <int MODE, int S, bool T64, int DYN, int OPT = 0>
 __global__ __launch_bounds__(1024) void k1(Args a) {
     __shared__ uint4 lds4[(T64 ? 65536 : 131072) / 16];
     if (MODE != 0) {
@@ -145,7 +188,7 @@ __global__ __launch_bounds__(1024) void k1(Args a) {
         for (uint32_t i = threadIdx.x; i < (T64 ? 65536u : 131072u) / 16u; i += 1024u) lds4[i] = src[i];
         __syncthreads();
     }
-    body<MODE, S, T64, DYN>(a, reinterpret_cast<const char *>(lds4));
+    body<MODE, S, T64, DYN, OPT>(a, reinterpret_cast<const char *>(lds4));
 }
 
 // two workgroups per CU: 8 waves per SIMD, at most 64 VGPRs
@@ -262,10 +305,9 @@ int main() {
     for (int round = 0; round < 2; ++round) {
         run("product", k1<1, 2, false, 0>, cus, tab128, 0, 2);
         run("loads", k1<0, 2, false, 0>, cus, tab128, 0, 2);
-        run("dynamic per-XCD tickets", k1<1, 2, false, 1>, cus, tab128, 1, 2);
-        run("dynamic per-workgroup tickets", k1<1, 2, false, 2>, cus, tab128, 2, 2);
-        run("loads, dynamic per-XCD tickets", k1<0, 2, false, 1>, cus, tab128, 1, 2);
-        run("s2 64K tables", k1<1, 2, true, 0>, cus, tab64, 0, 2);
+        run("product + setprio(3) around the load bursts", k1<1, 2, false, 0, 1>, cus, tab128, 0, 2);
+        run("product, next set's loads interleaved with the row steps", k1<1, 2, false, 0, 2>, cus, tab128, 0, 2);
+        run("S = 1, next packet's loads interleaved", k1<1, 1, false, 0, 2>, cus, tab128, 0, 1);
     }
     return 0;
 }

@@ -86,7 +86,7 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 13, 16, 20, 24, 25, 26, 40])
+@pytest.mark.parametrize("variant", [0, 13, 16, 17, 20, 24, 25, 26, 40])
 def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
@@ -982,7 +982,7 @@ def test_split_batches_concurrent_streams(engine):
 def test_kernel_variant_validation(engine):
     import icrc_amd
 
-    for v in (-1, 0, 13, 15, 16, 18, 19, 20, 24, 25, 26, 31, 32, 35, 40, 41, 42, 43, 44, 45, 46, 120, 124, 140, 146, 224, 240, 301):
+    for v in (-1, 0, 13, 15, 16, 17, 18, 19, 20, 24, 25, 26, 31, 32, 35, 40, 41, 42, 43, 44, 45, 46, 120, 124, 140, 146, 224, 240, 301):
         engine.set_variant(v)
     engine.set_variant(-1)
     for v in (-2, 1, 10, 14, 21, 27, 36, 47, 99, 100, 116, 147, 302, 400):
