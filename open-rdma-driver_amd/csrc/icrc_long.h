@@ -95,6 +95,8 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 // operand of the row loads (0 default, 2 nt: read-once stream).
 // kAblNoPrio: leave the wave priority alone around the load burst (A/B: variant 17).
 constexpr int kAblNoPrio = 1 << 8;
+// kAblNoFinal (diagnostic, variant 21): skip the per-lane final product M^(64-l) (wrong results)
+constexpr int kAblNoFinal = 1 << 9;
 constexpr int abl_mode(int abl) { return abl & 3; }
 constexpr int abl_aux(int abl) { return (abl >> 2) & 0x3F; }
 constexpr bool abl_prio(int abl) { return (abl & kAblNoPrio) == 0; }
@@ -333,7 +335,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         }
         uint32_t fin[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s) fin[s] = final_mul(lds, acc[s], c.fin);
+        for (int s = 0; s < S; ++s) fin[s] = (ABL & kAblNoFinal) ? acc[s] : final_mul(lds, acc[s], c.fin);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]),
