@@ -499,7 +499,9 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
             constexpr int b = decltype(bc)::value;
             constexpr int bp = (b + D) % B;
             next(m[bp][0], qs[bp]);
+            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(3);
             slot_load<ABL, MODE>(m[bp][0], lane, u[bp][0]);
+            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(0);
             if (m[bp][0].kind) inflight += 1;
             if (m[b][0].kind) {
                 const int blk = static_cast<int>(qs[b] >> 6);
