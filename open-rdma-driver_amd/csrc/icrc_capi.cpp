@@ -779,8 +779,17 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
         p.variant = rxv;
         return icrc::launch_rx(p, grid_for(e, n), stream);
     }
-    // Two passes (icrc_kernels.hip, icrc_rx_desc_kernel): the verify dispatch writes the ok bytes
-    // (into d_ok, or a stream-ordered scratch array when the caller passes none), then the
+    // Small batches (at most one packet per wave, e.g. a 16 MiB message): ONE pass, verify +
+    // descriptors (icrc_rx_kernel, descriptors collected per 64-packet block and stored with the
+    // results): 4096 x 4156 B in 12.1 us instead of 15.3, 256 x 316 B in 8.9 instead of 12.4
+    // (scripts/probe_rx_small.py).  On large batches the same fused pass measured slower than the
+    // two passes (786 K x 4156 B: 0.70 vs 0.59 ms, profiles/r02_rx_fused_ab.jsonl).
+    if (e->variant < 0 && n <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup) {
+        p.variant = 2;
+        return icrc::launch_rx(p, grid_for(e, n), stream);
+    }
+    // Otherwise two passes (icrc_kernels.hip, icrc_rx_desc_kernel): the verify dispatch writes the
+    // ok bytes (into d_ok, or a stream-ordered scratch array when the caller passes none), then the
     // descriptors are built from the header words and those bytes.
     p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
@@ -789,6 +798,7 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     if (!d_ok) HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&scratch), n, s));
     p.ok = d_ok ? d_ok : scratch;
     int rc = dispatch(e, icrc::kVerify, p, stream);
+    p.split_len = 0;
     if (rc == ICRC_OK) rc = icrc::launch_rx_desc(p, e->num_cu, stream);
     if (scratch && hipFreeAsync(scratch, s) != hipSuccess && rc == ICRC_OK) rc = ICRC_EDEVICE;
     return rc;

@@ -81,9 +81,11 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     }
 }
 
-// Receive: verify + strip + parse — the default pipelined path (variant 13) with the header
-// words gathered from each packet's first two rows.
-template <int S, int D, bool TRAILER>
+// Receive: verify + strip + parse in one pass over the one-packet pipeline, the header words
+// gathered from each packet's first two rows as loaded.  PARSE 2 (the default for small batches):
+// descriptors collected per 64-packet block and stored with its results (RxAcc, icrc_long.h);
+// PARSE 1 (A/B variant 301): a descriptor store per packet.
+template <int S, int D, bool TRAILER, int PARSE>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     {
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, S, D, kStreamAux << 2, 1, false, TRAILER>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, S, D, kStreamAux << 2, PARSE, false, TRAILER>(p, lds, c, lane, lo, nq);
 }
 
 // ---- receive parse, pass 2 (icrc_rx_parse_device default) ----------------------------------
@@ -185,48 +187,8 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
                 h[k] = x;
             }
         }
-        const bool valid = L >= ICRC_MIN_PACKET;
-        const uint32_t w7 = h[7], w9 = h[9], w10 = h[10];
-        const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
-        // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
-        const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
-                          : (op == 0x0Cu)                 ? 44u
-                          : (op == 0x11u)                 ? 16u
-                          : (op >= 0x06u && op <= 0x10u)  ? 28u
-                                                          : 0u;
-        const uint32_t status = !valid                  ? ICRC_RX_TRUNCATED
-                              : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
-                              : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
-                              : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
-                                                        : ICRC_RX_OK;
-        const bool ack = hs == 16u;
-        const bool ok = status == ICRC_RX_OK;
-        const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
-                               (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
-                               (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
-        const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
-        const uint64_t poff = off + 28u + hs;
-        // present classes: General metadata has a RETH, Acknowledge an AETH; none on error
-        const bool reth = ok && !ack, sec = ok && hs == 44u, imm = ok && hs == 32u, aeth = ok && ack;
         uint32_t v[18];
-        v[0] = reth ? bswap32(h[11]) : 0u;  // RETH va (big-endian u64, bytes 40-47)
-        v[1] = reth ? bswap32(h[10]) : 0u;
-        v[2] = sec ? bswap32(h[15]) : 0u;   // secondary RETH va (bytes 56-63)
-        v[3] = sec ? bswap32(h[14]) : 0u;
-        v[4] = ok ? static_cast<uint32_t>(poff) : 0u;
-        v[5] = ok ? static_cast<uint32_t>(poff >> 32) : 0u;
-        v[6] = ok ? L - 32u - hs - pad : 0u;
-        v[7] = reth ? bswap32(h[12]) : 0u;  // rkey, dlen
-        v[8] = reth ? bswap32(h[13]) : 0u;
-        v[9] = sec ? bswap32(h[16]) : 0u;
-        v[10] = sec ? bswap32(h[17]) : 0u;
-        v[11] = imm ? bswap32(h[14]) : 0u;
-        v[12] = ok ? bswap32(h[8]) & 0xFFFFFFu : 0u;     // dqpn
-        v[13] = ok ? bswap32(h[9]) & 0xFFFFFFu : 0u;     // psn
-        v[14] = aeth ? bswap32(h[10]) & 0xFFFFFFu : 0u;  // AETH msn
-        v[15] = ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u;
-        v[16] = ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u;
-        v[17] = (okb & 0xFFu) | (status << 8);
+        rx_decode(h, off, L, okb, v);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (uint32_t k = 0; k < 18; ++k) sh[lane * kRxStride + k] = v[k];
@@ -876,9 +838,16 @@ int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.n == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    // A/B only (variant 301): the fused single-pass receive, S = 2, D = 1
-    if (p.trailer) hipLaunchKernelGGL((icrc_rx_kernel<2, 1, true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
-    else hipLaunchKernelGGL((icrc_rx_kernel<2, 1, false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    // p.variant 1 (A/B variant 301): a descriptor store per packet; otherwise descriptors per block
+#define ICRC_RX(T, P) hipLaunchKernelGGL((icrc_rx_kernel<2, 1, T, P>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+    if (p.variant == 1) {
+        if (p.trailer) ICRC_RX(true, 1);
+        else ICRC_RX(false, 1);
+    } else {
+        if (p.trailer) ICRC_RX(true, 2);
+        else ICRC_RX(false, 2);
+    }
+#undef ICRC_RX
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -263,14 +263,165 @@ __device__ __forceinline__ void head_masks_init(HeadMasks &hm) {
     hm.m0 = hm.m1 = 0;
 }
 
+// Lane = packet decode of one receive descriptor (to_rdma_message, packet_processor.rs:18-71, on
+// the UDP payload with the ICRC stripped; field getters packet.rs:57-98 BTH, 173-183 RETH, 222-232
+// AETH, 249-251 Immediate).  h[k] = packet word k (bytes 4k..4k+3, LE), zero where the packet has
+// no such word before its trailer (words 0..6, IPv4 and UDP, are not read); okb = the verify
+// result byte.  v = the 18 dwords of
+// icrc_rx_desc.  Shared by the descriptor pass (icrc_rx_desc_kernel) and the fused parse below.
+__device__ __forceinline__ void rx_decode(const uint32_t (&h)[18], uint64_t off, uint32_t L, uint32_t okb,
+                                          uint32_t (&v)[18]) {
+    const bool valid = L >= ICRC_MIN_PACKET;
+    const uint32_t w7 = h[7], w9 = h[9], w10 = h[10];
+    const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+    // header struct size per opcode (packet.rs:427-438): BthReth 28, +Imm 32, DoubleReth 44, Aeth 16
+    const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                      : (op == 0x0Cu)                 ? 44u
+                      : (op == 0x11u)                 ? 16u
+                      : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                      : 0u;
+    const uint32_t status = !valid                  ? ICRC_RX_TRUNCATED
+                          : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
+                          : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
+                          : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED  // buf_size = L - 28 - 4
+                                                    : ICRC_RX_OK;
+    const bool ack = hs == 16u;
+    const bool ok = status == ICRC_RX_OK;
+    const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                           (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                           (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+    const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+    const uint64_t poff = off + 28u + hs;
+    // present classes: General metadata has a RETH, Acknowledge an AETH; none on error
+    const bool reth = ok && !ack, sec = ok && hs == 44u, imm = ok && hs == 32u, aeth = ok && ack;
+    v[0] = reth ? bswap32(h[11]) : 0u;  // RETH va (big-endian u64, bytes 40-47)
+    v[1] = reth ? bswap32(h[10]) : 0u;
+    v[2] = sec ? bswap32(h[15]) : 0u;   // secondary RETH va (bytes 56-63)
+    v[3] = sec ? bswap32(h[14]) : 0u;
+    v[4] = ok ? static_cast<uint32_t>(poff) : 0u;
+    v[5] = ok ? static_cast<uint32_t>(poff >> 32) : 0u;
+    v[6] = ok ? L - 32u - hs - pad : 0u;
+    v[7] = reth ? bswap32(h[12]) : 0u;  // rkey, dlen
+    v[8] = reth ? bswap32(h[13]) : 0u;
+    v[9] = sec ? bswap32(h[16]) : 0u;
+    v[10] = sec ? bswap32(h[17]) : 0u;
+    v[11] = imm ? bswap32(h[14]) : 0u;
+    v[12] = ok ? bswap32(h[8]) & 0xFFFFFFu : 0u;     // dqpn
+    v[13] = ok ? bswap32(h[9]) & 0xFFFFFFu : 0u;     // psn
+    v[14] = aeth ? bswap32(h[10]) & 0xFFFFFFu : 0u;  // AETH msn
+    v[15] = ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u;
+    v[16] = ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u;
+    v[17] = (okb & 0xFFu) | (status << 8);
+}
+
+// PARSE = 2, the fused receive parse of the one-packet pipeline (small batches, icrc_rx_kernel):
+// no store per packet (a store in the ring makes hipcc wait for zero there, draining the prefetch).  Each packet's header words
+// (lane w = word w, from its rows as loaded), offset and length go into lane q & 63 of these
+// registers (v_readlane / v_writelane, uniform lanes); when the 64-packet block's results leave,
+// the block is decoded lane = packet (rx_decode) and its descriptors leave with them, as 18 buffer
+// stores (lanes without a packet of this kernel out of range).
+// Only words 7..17 are kept (BTH from byte 28, extension headers): the decode reads no IPv4 / UDP
+// word, and every register here is one fewer for the ring.
+constexpr int kRxW0 = 7, kRxWords = 18 - kRxW0;
+struct RxAcc {
+    uint32_t h[kRxWords];  // h[k - kRxW0] = packet word k
+    uint32_t off_lo, off_hi, len;
+    uint64_t have;  // block lanes holding a packet
+};
+
+__device__ __forceinline__ void rx_acc_init(RxAcc &a) {
+#pragma unroll
+    for (int k = 0; k < kRxWords; ++k) a.h[k] = 0u;
+    a.off_lo = a.off_hi = a.len = 0u;
+    a.have = 0ull;
+}
+
+// old with lane l replaced by v (v and l wave-uniform).  hipcc has no builtin for v_writelane_b32;
+// the LLVM intrinsic is bound by name (the backend puts the lane select in m0, as gfx9's one
+// constant-bus read per VALU op requires).
+extern "C" __device__ int icrc_llvm_writelane(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t writelane_u32(uint32_t v, uint32_t l, uint32_t old) {
+    return static_cast<uint32_t>(icrc_llvm_writelane(static_cast<int>(v), static_cast<int>(l), static_cast<int>(old)));
+}
+
+// hdr: packet word w in lane w (w < 18); words at or past the trailer (4 w + 8 > L) are dropped.
+__device__ __forceinline__ void rx_acc_put(RxAcc &a, uint32_t hdr, uint32_t qb, uint64_t off, uint32_t L) {
+    // word k to lane qb: one ds_bpermute per word would also do; a lane select keeps it in VALU
+    const bool me = __lane_id() == qb;
+#pragma unroll
+    for (int k = kRxW0; k < 18; ++k) {
+        const uint32_t w = 4u * static_cast<uint32_t>(k) + 8u <= L ? readlane_u32(hdr, k) : 0u;
+        a.h[k - kRxW0] = me ? w : a.h[k - kRxW0];
+    }
+    a.off_lo = me ? static_cast<uint32_t>(off) : a.off_lo;
+    a.off_hi = me ? static_cast<uint32_t>(off >> 32) : a.off_hi;
+    a.len = me ? L : a.len;
+    a.have |= 1ull << qb;
+}
+
+// The block's descriptors (packets base .. base + 63; okv lane q = packet q's verify result).
+// Every lane issues every store (out of range without a packet): no branch around a store.  The
+// fields follow rx_decode; each dword is formed just before its store (sched_barrier) so the flush
+// needs few registers beside the ring's.
+__device__ __forceinline__ void rx_acc_flush(const BatchParams &p, RxAcc &a, uint32_t base, uint32_t okv, uint32_t lane) {
+    const uint32_t L = a.len;
+    const uint32_t w7 = a.h[7 - kRxW0], w9 = a.h[9 - kRxW0], w10 = a.h[10 - kRxW0];
+    const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, fl = (w7 >> 8) & 0xFFu, pad = (fl >> 5) & 3u;
+    const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                      : (op == 0x0Cu)                 ? 44u
+                      : (op == 0x11u)                 ? 16u
+                      : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                      : 0u;
+    const uint32_t status = (L < ICRC_MIN_PACKET)   ? ICRC_RX_TRUNCATED
+                          : (hs == 0u)              ? ICRC_RX_INVALID_OPCODE
+                          : (tran > 6u)             ? ICRC_RX_INVALID_TRANS_TYPE
+                          : (L - 32u < hs + pad)    ? ICRC_RX_TRUNCATED
+                                                    : ICRC_RX_OK;
+    const bool ack = hs == 16u, ok = status == ICRC_RX_OK;
+    const bool reth = ok && !ack, sec = ok && hs == 44u, imm = ok && hs == 32u, aeth = ok && ack;
+    const uint64_t poff = (static_cast<uint64_t>(a.off_lo) | (static_cast<uint64_t>(a.off_hi) << 32)) + 28u + hs;
+    const bool mine = (a.have >> lane) & 1ull;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint8_t *>(p.rx + base), 0, static_cast<int>(64u * sizeof(icrc_rx_desc)), 0x00020000);
+    auto st = [&](int k, uint32_t v) __attribute__((always_inline)) {
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, static_cast<int>(mine ? lane * 72u + 4u * k : 0x80000000u), 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto hw = [&](int k) __attribute__((always_inline)) { return a.h[k - kRxW0]; };
+    st(0, reth ? bswap32(hw(11)) : 0u);  // RETH va (big-endian u64, bytes 40-47)
+    st(1, reth ? bswap32(hw(10)) : 0u);
+    st(2, sec ? bswap32(hw(15)) : 0u);   // secondary RETH va (bytes 56-63)
+    st(3, sec ? bswap32(hw(14)) : 0u);
+    st(4, ok ? static_cast<uint32_t>(poff) : 0u);
+    st(5, ok ? static_cast<uint32_t>(poff >> 32) : 0u);
+    st(6, ok ? L - 32u - hs - pad : 0u);
+    st(7, reth ? bswap32(hw(12)) : 0u);  // rkey, dlen
+    st(8, reth ? bswap32(hw(13)) : 0u);
+    st(9, sec ? bswap32(hw(16)) : 0u);
+    st(10, sec ? bswap32(hw(17)) : 0u);
+    st(11, imm ? bswap32(hw(14)) : 0u);
+    st(12, ok ? bswap32(hw(8)) & 0xFFFFFFu : 0u);     // dqpn
+    st(13, ok ? bswap32(w9) & 0xFFFFFFu : 0u);        // psn
+    st(14, aeth ? bswap32(w10) & 0xFFFFFFu : 0u);     // AETH msn
+    st(15, ok ? (bswap16(w7 >> 16) | (op << 16) | (tran << 24)) : 0u);
+    const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                           (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                           (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+    const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+    st(16, ok ? (flags | (pad << 8) | (code << 16) | (value << 24)) : 0u);
+    st(17, (okv & 0xFFu) | (status << 8));
+    a.have = 0ull;
+}
+
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
 // the wave's result buffer.
-// PARSE: 0 off; 1 receive parse (rx_store).
+// PARSE: 0 off; 1 receive parse, a descriptor store per packet (rx_store; A/B variant 301);
+// 2 receive parse into RxAcc (the default fused receive).
 template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
                                             uint32_t lane, const SlotMeta (&m)[S],
                                             uint32_t (&u)[S][ring_words<MODE>()], uint32_t q0, ResultBuf &rb,
-                                            HeadMasks &hm, uint32_t lo = 0) {
+                                            HeadMasks &hm, RxAcc &ra, uint32_t lo = 0) {
     int rmax = 0;
     bool same = true;  // every slot regular with the same row count (the common case)
 #pragma unroll
@@ -284,6 +435,12 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         if constexpr (PARSE) {
 #pragma unroll
             for (int s = 0; s < S; ++s) hdr[s] = rx_gather_header(u[s][0], u[s][1], m[s].k0, lane);
+        }
+        if constexpr (PARSE == 2) {  // into RxAcc now, so hdr is not live across the row steps
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+                if (m[s].kind == 1)
+                    rx_acc_put(ra, hdr[s], (q0 + s) & 63u, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L);
         }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
@@ -342,7 +499,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                                                              MODE == kVerify ? u[s][ring_words<MODE>() - 1] : 0u, lane);
             if (m[s].kind == 1) {
                 rb_put(rb, q0 + s, r);
-                if constexpr (PARSE)
+                if constexpr (PARSE == 1)
                     rx_store(p.rx, lo + q0 + s, hdr[s], static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
             }
         }
@@ -354,8 +511,10 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             if constexpr (PARSE) hdr_slow = rx_header_bytes(m[s].pkt, m[s].L, lane);  // before any trailer zeroing
             const uint32_t r = handle_packet<MODE>(p, m[s].pkt, m[s].L, lds, c, lane);
             rb_put(rb, q0 + s, r);
-            if constexpr (PARSE)
+            if constexpr (PARSE == 1)
                 rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
+            if constexpr (PARSE == 2)
+                rx_acc_put(ra, hdr_slow, (q0 + s) & 63u, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L);
         }
 }
 
@@ -379,6 +538,8 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     rb.valid = 0;
     HeadMasks hm;
     head_masks_init(hm);
+    RxAcc ra;
+    if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
 #pragma unroll
@@ -409,9 +570,12 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             }
             if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(0);
             const uint32_t q0 = ts * S;
-            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, lo);
+            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, ra, lo);
             const uint32_t qn = q0 + S;  // next unprocessed
-            if ((qn & 63u) == 0 || qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+            if ((qn & 63u) == 0 || qn >= nq) {
+                if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
+                rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+            }
             return true;
         });
         if (!cont) return;
@@ -444,6 +608,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     int rb_block = -1;
     HeadMasks hm;
     head_masks_init(hm);
+    RxAcc ra;  // unused (no parse here)
     SlotMeta m[B][1];
     uint32_t qs[B];
     uint32_t u[B][1][ring_words<MODE>()];
@@ -509,7 +674,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
                     if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
                     rb_block = blk;
                 }
-                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, lo);
+                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
                 inflight -= 1;
             }
             return true;

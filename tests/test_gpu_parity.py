@@ -634,7 +634,7 @@ def assert_desc_equal(got, want):
         np.testing.assert_array_equal(got[f], want[f], err_msg=f)
 
 
-@pytest.mark.parametrize("rx_variant", [-1, 301])  # two-pass default, fused single pass
+@pytest.mark.parametrize("rx_variant", [-1, 16, 301])  # default (a small batch: one fused pass), two passes, per-packet stores
 @pytest.mark.parametrize("layout", ["packed", "aligned"])
 @pytest.mark.parametrize("zero_trailer", [False, True])
 def test_rx_parse_matches_oracle(engine, layout, zero_trailer, rx_variant):
@@ -667,6 +667,47 @@ def _rx_parse_case(engine, layout, zero_trailer, rx_cases):
     np.testing.assert_array_equal(ok, want["icrc_ok"])
     assert nerr == int(np.sum(np.asarray(sizes) < 44))
     np.testing.assert_array_equal(after, ref)
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+@pytest.mark.parametrize("zero_trailer", [False, True])
+def test_rx_parse_small_batch_boundary(engine, extra, zero_trailer):
+    """The default receive takes batches of at most one packet per wave in ONE fused pass
+    (descriptors collected per 64-packet block) and larger ones in two passes: both sides of the
+    boundary (#CUs x 16 packets, and one more), a 16 MiB WRITE's packets with mixed lengths and
+    misaligned ones, one flipped bit per 97 packets."""
+    import icrc_amd
+
+    n = torch.cuda.get_device_properties(0).multi_processor_count * 16 + extra
+    rng = np.random.default_rng(11 + extra)
+    buf, off, lens = oracle.synth_middle_stream(n, psn0=0x10)
+    # ragged: some packets shortened to other MTU classes / odd lengths (pad), a few misaligned
+    pkts = [buf[int(o): int(o) + int(L)].copy() for o, L in zip(off, lens)]
+    for i in rng.choice(n, n // 8, replace=False):
+        L = int(rng.choice([60, 61, 316, 1084, 2001]))
+        p = pkts[i][:L].copy()
+        p[2:4] = np.frombuffer(int(L).to_bytes(2, "big"), np.uint8)
+        pkts[i] = p
+    sizes = np.array([p.size for p in pkts], np.uint32)
+    gaps = rng.integers(0, 4, n) * (rng.random(n) < 0.05)  # 5 % start off a word boundary
+    offs = np.zeros(n, np.uint64)
+    pos = 0
+    for i, p in enumerate(pkts):
+        pos += int(gaps[i])
+        offs[i] = pos
+        pos += p.size
+    b = np.zeros(pos + 8, np.uint8)
+    for o, p in zip(offs, pkts):
+        b[int(o): int(o) + p.size] = p
+    for i in range(0, n, 97):
+        b[int(offs[i]) + 50] ^= 0x01
+    ref = b.copy()
+    want = oracle.rx_parse(ref, offs, sizes, zero_trailer=zero_trailer)
+    got, ok, nerr, after = run_rx(engine, b, offs, sizes, zero_trailer)
+    assert_desc_equal(got, want)
+    np.testing.assert_array_equal(ok, want["icrc_ok"])
+    np.testing.assert_array_equal(after, ref)
+    assert icrc_amd.RX_DESC_DTYPE.itemsize == 72
 
 
 @pytest.mark.parametrize("ragged", [False, True])
