@@ -134,9 +134,11 @@ int icrc_verify_strided_device(icrc_engine *engine, uint8_t *d_base, uint64_t st
  * PacketProcessor::to_rdma_message (packet_processor.rs:18-71, packet.rs:286-438) applied to the
  * UDP payload with the ICRC stripped (pkt[28 .. L-4)): the emulator hands the whole datagram,
  * trailer included, to to_rdma_message (device_inner.rs:150) and so reports payloads 4 bytes
- * too long; here payload_len excludes it.  Two kernels on `stream`: the verify batch, then a
- * descriptor pass that re-reads each packet's first 72 bytes.  With d_ok NULL the
- * ok bytes go to a stream-ordered scratch array (hipMallocAsync / hipFreeAsync on `stream`). */
+ * too long; here payload_len excludes it.  A batch of at most one packet per wave (#CUs x 16)
+ * runs as ONE fused kernel; larger ones as two kernels on `stream`: the verify batch, then a
+ * descriptor pass that re-reads each packet's first 72 bytes.  With d_ok NULL
+ * the two-kernel form keeps the ok bytes in a stream-ordered scratch array (hipMallocAsync /
+ * hipFreeAsync on `stream`). */
 #define ICRC_RX_OK 0u
 #define ICRC_RX_INVALID_OPCODE 1u     /* PacketError::InvalidOpcode (opcode not in 0x06..0x11)   */
 #define ICRC_RX_INVALID_TRANS_TYPE 2u /* PacketError::FailedToConvertTransType (tran_type > 6) */
