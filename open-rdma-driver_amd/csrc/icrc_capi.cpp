@@ -651,7 +651,7 @@ int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : IC
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
     const bool hybrid = icrc::is_short_variant(variant - icrc::kHybridVariantBase) ||
                         icrc::is_short_variant(variant - icrc::kHybridCompactBase);
-    const bool rx = variant == icrc::kRxVariantBase + 1;
+    const bool rx = variant > icrc::kRxVariantBase && variant <= icrc::kRxVariantBase + 4;
     if (!e || (variant != -1 && !icrc::is_batch_variant(variant) && !hybrid && !rx)) return ICRC_EINVAL;
     e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;
@@ -775,7 +775,7 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     p.trailer = zero_trailer ? 1 : 0;
     p.rx = d_desc;
     const int rxv = e->variant >= icrc::kRxVariantBase ? e->variant - icrc::kRxVariantBase : 0;
-    if (rxv != 0) {  // A/B: the fused single-pass kernel
+    if (rxv != 0) {  // A/B: the fused single-pass kernel on any batch (301: a store per packet, 302: per block)
         p.variant = rxv;
         return icrc::launch_rx(p, grid_for(e, n), stream);
     }

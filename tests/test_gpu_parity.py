@@ -711,7 +711,7 @@ def test_rx_parse_small_batch_boundary(engine, extra, zero_trailer):
 
 
 @pytest.mark.parametrize("ragged", [False, True])
-@pytest.mark.parametrize("rx_variant", [-1, 301])
+@pytest.mark.parametrize("rx_variant", [-1, 301, 302])
 def test_rx_parse_c1_stream(engine, ragged, rx_variant):
     """A 4 KiB WRITE_MIDDLE stream (strided, or the same packets through offset / length arrays) with
     one flipped bit per 1024; the ok bytes go to d_ok as well.  70 000 packets: every wave of the
@@ -1023,10 +1023,10 @@ def test_split_batches_concurrent_streams(engine):
 def test_kernel_variant_validation(engine):
     import icrc_amd
 
-    for v in (-1, 0, 13, 15, 16, 17, 18, 19, 20, 21, 24, 25, 26, 31, 32, 35, 40, 41, 42, 43, 44, 45, 46, 120, 124, 140, 146, 224, 240, 301):
+    for v in (-1, 0, 13, 15, 16, 17, 18, 19, 20, 21, 24, 25, 26, 31, 32, 35, 40, 41, 42, 43, 44, 45, 46, 120, 124, 140, 146, 224, 240, 301, 302):
         engine.set_variant(v)
     engine.set_variant(-1)
-    for v in (-2, 1, 10, 14, 22, 27, 36, 47, 99, 100, 116, 147, 302, 400):
+    for v in (-2, 1, 10, 14, 22, 27, 36, 47, 99, 100, 116, 147, 305, 400):
         with pytest.raises(icrc_amd.IcrcError) as e:
             engine.set_variant(v)
         assert e.value.rc == icrc_amd.EINVAL
