@@ -651,7 +651,7 @@ int icrc_engine_device_ordinal(const icrc_engine *e) { return e ? e->device : IC
 int icrc_engine_set_kernel_variant(icrc_engine *e, int variant) {
     const bool hybrid = icrc::is_short_variant(variant - icrc::kHybridVariantBase) ||
                         icrc::is_short_variant(variant - icrc::kHybridCompactBase);
-    const bool rx = variant > icrc::kRxVariantBase && variant <= icrc::kRxVariantBase + 4;
+    const bool rx = variant == icrc::kRxVariantBase + 1 || variant == icrc::kRxVariantBase + 2;
     if (!e || (variant != -1 && !icrc::is_batch_variant(variant) && !hybrid && !rx)) return ICRC_EINVAL;
     e->variant = variant < 0 ? -1 : variant;
     return ICRC_OK;

@@ -843,10 +843,6 @@ int launch_rx(const BatchParams &p, int grid, void *stream) {
     if (p.variant == 1) {
         if (p.trailer) ICRC_RX(true, 1);
         else ICRC_RX(false, 1);
-    } else if (p.variant == 3) {  // diagnostics (variants 303 / 304)
-        ICRC_RX(false, 3);
-    } else if (p.variant == 4) {
-        ICRC_RX(false, 4);
     } else {
         if (p.trailer) ICRC_RX(true, 2);
         else ICRC_RX(false, 2);

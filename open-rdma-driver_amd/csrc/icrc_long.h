@@ -422,8 +422,7 @@ __device__ __forceinline__ void rx_acc_flush(const BatchParams &p, RxAcc &a, uin
 // Process one set of S packets (wave-local sequence numbers q0 .. q0+S-1); results go to
 // the wave's result buffer.
 // PARSE: 0 off; 1 receive parse, a descriptor store per packet (rx_store; A/B variant 301);
-// 2 receive parse into RxAcc (the fused receive of small batches); diagnostics: 3 = 2 without the
-// descriptor stores, 4 = 2 without the per-packet header moves (wrong descriptors).
+// 2 receive parse into RxAcc (the fused receive of small batches).
 template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
                                             uint32_t lane, const SlotMeta (&m)[S],
@@ -443,7 +442,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 #pragma unroll
             for (int s = 0; s < S; ++s) hdr[s] = rx_gather_header(u[s][0], u[s][1], m[s].k0, lane);
         }
-        if constexpr (PARSE == 2 || PARSE == 3) {  // into RxAcc now, so hdr is not live across the row steps
+        if constexpr (PARSE == 2) {  // into RxAcc now, so hdr is not live across the row steps
 #pragma unroll
             for (int s = 0; s < S; ++s)
                 if (m[s].kind == 1)
@@ -520,7 +519,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             rb_put(rb, q0 + s, r);
             if constexpr (PARSE == 1)
                 rx_store(p.rx, lo + q0 + s, hdr_slow, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L, r, lane, c);
-            if constexpr (PARSE >= 2)
+            if constexpr (PARSE == 2)
                 rx_acc_put(ra, hdr_slow, (q0 + s) & 63u, static_cast<uint64_t>(m[s].pkt - p.base), m[s].L);
         }
 }
@@ -546,7 +545,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     HeadMasks hm;
     head_masks_init(hm);
     RxAcc ra;
-    if constexpr (PARSE >= 2) rx_acc_init(ra);
+    if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
 #pragma unroll
@@ -580,8 +579,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, ra, lo);
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) {
-                if constexpr (PARSE == 2 || PARSE == 4) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
-                if constexpr (PARSE == 3) ra.have = 0;  // diagnostic: no descriptor stores
+                if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
                 rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             }
             return true;
