@@ -67,7 +67,7 @@ constexpr int kRxVariantBase = 300;
 // are diagnostics whose results are wrong by design.
 inline bool is_batch_variant(int v) {
     switch (v) {
-    case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 24: case 25: case 26: case 31: case 32: case 35:
+    case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 24: case 25: case 26: case 31: case 32: case 35:
     case 40: case 41: case 42: case 43: case 44: case 45: case 46:
         return true;
     default:

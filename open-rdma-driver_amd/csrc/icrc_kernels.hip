@@ -776,6 +776,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 19: ICRC_LAUNCH(2, 1, 1 | (2 << 2), false); break;  // diagnostic: loads only of the default (16) ring
     case 17: ICRC_LAUNCH_T(2, 1, (2 << 2) | kAblNoPrio); break;  // 16 without the raised priority (A/B)
     case 21: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoFinal, false); break;  // diagnostic: 16 without final products
+    case 22: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoStore, false); break;  // diagnostic: 16 without result stores
     case 20:
     case 24:
     case 25:

@@ -97,6 +97,8 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 constexpr int kAblNoPrio = 1 << 8;
 // kAblNoFinal (diagnostic, variant 21): skip the per-lane final product M^(64-l) (wrong results)
 constexpr int kAblNoFinal = 1 << 9;
+// kAblNoStore (diagnostic, variant 22): no result stores (nothing written)
+constexpr int kAblNoStore = 1 << 10;
 constexpr int abl_mode(int abl) { return abl & 3; }
 constexpr int abl_aux(int abl) { return (abl >> 2) & 0x3F; }
 constexpr bool abl_prio(int abl) { return (abl & kAblNoPrio) == 0; }
@@ -580,7 +582,8 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) {
                 if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
-                rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+                if constexpr ((ABL & kAblNoStore) == 0) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+                else rb.valid = 0;
             }
             return true;
         });
