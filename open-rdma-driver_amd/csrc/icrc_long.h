@@ -97,7 +97,7 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 constexpr int kAblNoPrio = 1 << 8;
 // kAblNoFinal (diagnostic, variant 21): skip the per-lane final product M^(64-l) (wrong results)
 constexpr int kAblNoFinal = 1 << 9;
-// kAblNoStore (diagnostic, variant 22): no result stores (nothing written)
+// kAblNoStore (diagnostic, variant 22): the result stores of every block but the chunk's last
 constexpr int kAblNoStore = 1 << 10;
 constexpr int abl_mode(int abl) { return abl & 3; }
 constexpr int abl_aux(int abl) { return (abl >> 2) & 0x3F; }
@@ -582,8 +582,10 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) {
                 if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
+                // kAblNoStore: only the chunk's last block is stored (its lanes depend on every
+                // earlier packet through rb_put's selects, so nothing is dead code)
                 if constexpr ((ABL & kAblNoStore) == 0) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
-                else rb.valid = 0;
+                else if (qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             }
             return true;
         });
