@@ -346,6 +346,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     auto issue = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
         OctSlot<MODE, TRAILER> &S = sl[b];
+        if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(3);  // the frame's setup gates its loads
         if (lt >= lnfr) {  // the block is issued: the next one, if prepared
             if (nb_ready) {
                 LB = NB;
@@ -391,7 +392,6 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             // Rows past a packet's end read the bytes after it (bounded by the block's extent) and
             // are never stepped: cheaper than a per-row descriptor select, and those bytes are the
             // block's next packets (L2-resident).
-            if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(3);  // the loads go out ahead of other waves' ALU work
             S.u[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o0), 0, 0);
 #pragma unroll
             for (int j = 1; j < K; ++j)
