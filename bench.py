@@ -85,17 +85,34 @@ def _free_port() -> int:
     return port
 
 
+def _shard_module():
+    """icrc_amd/shard.py loaded on its own: importing the icrc_amd package would load the HIP
+    library (its static constructors register kernels) in the launching process."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "_icrc_shard_launcher", os.path.join(ROOT, "open-rdma-driver_amd", "icrc_amd", "shard.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = mod  # dataclasses resolve their module through sys.modules
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def launch_ranks(args, argv) -> int:
     """--gpus N > 1 without torch.distributed.run around us: start it as a child process (no
-    exec, nothing has touched a GPU here) and return its exit status."""
+    exec, nothing has touched a GPU here: the GPUs are counted from the KFD topology or amdsmi,
+    never through HIP) and return its exit status."""
     if not args.cpu_stub:
-        import torch  # device_count() does not initialise the GPU on this image
-
-        have = torch.cuda.device_count()
+        try:
+            have, how = _shard_module().visible_gpu_count()
+        except RuntimeError as e:
+            log(f"bench.py: {e}; refusing to launch {args.gpus} ranks")
+            return 2
         if have < args.gpus:
-            log(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible; refusing to report a "
+            log(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible ({how}); refusing to report a "
                 f"{have}-GPU number as {args.gpus}")
             return 2
+        log(f"bench.py: {have} GPU(s) visible ({how})")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
@@ -180,6 +197,9 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     from icrc_amd import shard, workloads
 
     eng = icrc_amd.Engine(local)
+    if eng.ordinal != local:
+        log(f"bench.py: rank {rank}: engine on device {eng.ordinal}, expected LOCAL_RANK {local}")
+        return 2
     stream = torch.cuda.current_stream().cuda_stream
 
     # ---- C1 workload: weak = one QP stream per rank; strong = a shard of one stream ----
@@ -201,12 +221,17 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     wall, kms = time_kernel(step, args.steps, args.warmup, world)
     bytes_per_step = n * L
     # SURVEY 8(d) secondary denominator, same box and batch, after the timed region: the
-    # kernel's loads-only build (variant 19: the same row loads, ring and waits, no CRC)
-    eng.set_variant(LOADS_ONLY_VARIANT)
-    _, loads_ms = time_kernel(step, min(args.steps, 20), 3, world)
-    eng.set_variant(-1)
-    step()  # the loads-only build wrote its own values into d_out: restore the ICRCs for the check
+    # kernel's loads-only build (variant 19 of the A/B library: the same row loads, ring and waits,
+    # no CRC), into a scratch array (its results are wrong by design)
+    ab = icrc_amd.Engine(local, lib=icrc_amd.ab_library())
+    ab.set_variant(LOADS_ONLY_VARIANT)
+    d_scratch = torch.zeros(n, dtype=torch.int32, device="cuda")
+    _, loads_ms = time_kernel(lambda: ab.compute_strided(d_buf.data_ptr(), L, L, n, d_scratch.data_ptr(), False, stream),
+                              min(args.steps, 20), 3, world)
     torch.cuda.synchronize()
+    ab.close()
+    del d_scratch
+    per_rank = shard.gather_floats([kms, eng.ordinal, wall / args.steps * 1e3, loads_ms])
 
     # ---- CPU leg (outside the timed region): the parity sample on every rank; the CPU
     # baseline on rank 0 at N = 1.  The oracle is the checker / CPU port here only. ----
@@ -256,11 +281,13 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
                 "GB/s": round(bytes_per_step / (loads_ms * 1e-3) / 1e9, 1),
                 "kernel_ms": round(loads_ms, 4),
                 "frac": round(loads_ms / kms, 4),
-                "source": "the same kernel's loads-only build (variant 19: same row loads and ring, no "
-                          "CRC) on the same batch, timed after the K steps; frac = achieved / achievable",
+                "source": "the same kernel's loads-only build (variant 19 of the A/B library "
+                          "libicrc_amd_ab.so: same row loads and ring, no CRC) on the same batch, timed after "
+                          "the K steps; frac = achieved / achievable",
             },
         },
         "parity_sample": {"packets_checked_per_rank": checked, "failures_all_ranks": agg.failures},
+        "per_rank": per_rank_fields(per_rank),
     }
     tr = pmc_traffic(n, L)
     if tr is not None:
@@ -287,6 +314,20 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     return 0
 
 
+def per_rank_fields(rows):
+    """Rank-0 summary of every rank's [kernel ms, device ordinal, wall ms per step, loads-only ms]
+    (shard.gather_floats): a slow GPU or an imbalance shows here, not only in the max."""
+    kms = [r[0] for r in rows]
+    return {
+        "kernel_ms": [round(x, 4) for x in kms],
+        "device": [int(r[1]) for r in rows],
+        "wall_ms_per_step": [round(r[2], 4) for r in rows],
+        "loads_only_ms": [round(r[3], 4) for r in rows],
+        "kernel_ms_min": round(min(kms), 4),
+        "kernel_ms_max": round(max(kms), 4),
+    }
+
+
 def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_rank: int):
     """Rank-local parity: the first and last k packets of this rank's batch against the CPU
     restatement.  Returns (mismatches, packets checked)."""
@@ -308,7 +349,7 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
 
 
 PMC_TRAFFIC_FILE = "r02_pmc_traffic.json"
-LOADS_ONLY_VARIANT = 19  # icrc_batch_kernel<.., S = 2, D = 1, loads only>: the default ring without the CRC
+LOADS_ONLY_VARIANT = 19  # A/B library: icrc_batch_kernel<.., S = 2, D = 1, loads only>, the default ring without the CRC
 
 
 def pmc_traffic(n: int, L: int):
@@ -487,6 +528,7 @@ def extra_measurements(eng, stream, args, world):
 
     ex.update(fused_send_receive(eng, stream, args, world))
     ex.update(host_resident(eng, stream, args))
+    ex.update(host_message_c0(eng, stream, args))
     return ex
 
 
@@ -595,6 +637,76 @@ def host_resident(eng, stream, args):
     return ex
 
 
+def host_message_c0(eng, stream, args):
+    """configs[0]-shaped messages through the host-resident drop-ins, per message: one QP's 256 KiB
+    RDMA WRITE (64 x 4156-B packets, FIRST + 62 MIDDLE + LAST) in host memory, the send side's
+    icrc_compute_batch(write_trailer=1) (PacketWriter::write stores the ICRC, packet_processor.rs:
+    260-263) then the receive side's icrc_verify_batch(zero_trailer=1) (is_icrc_valid,
+    packet_processor.rs:341-353; udp_agent.rs:99) — what the emulator's send and receive threads
+    would call per message (queues/send/operations/write.rs:31-96).  Pinned and pageable buffers,
+    from 1 and 3 threads (each thread its own message buffer, the default engine shared, as the
+    reference's three callers would).  p50 / p99 microseconds per message (compute + verify)."""
+    import threading
+
+    import torch
+
+    import icrc_amd
+    from icrc_amd import workloads
+
+    w = workloads.write_message(256 << 10, 4096)
+    d_buf = workloads.synthesize(eng, w, stream=stream)
+    torch.cuda.synchronize()
+    src = d_buf.cpu().numpy()
+    off, lens = np.ascontiguousarray(w.off, np.uint64), np.ascontiguousarray(w.lens, np.uint32)
+    nbytes = int(lens.astype(np.uint64).sum())
+    reps = max(200, args.steps * 4)
+    out = {}
+    for kind in ("pinned", "pageable"):
+        for nth in (1, 3):
+            bufs = []
+            for _ in range(nth):
+                if kind == "pinned":
+                    t = torch.empty(src.size, dtype=torch.uint8, pin_memory=True)
+                    b = t.numpy()
+                    b[:] = src
+                    bufs.append((t, b))
+                else:
+                    bufs.append((None, src.copy()))
+            lat = [[] for _ in range(nth)]
+            bad = [0] * nth
+            gate = threading.Barrier(nth)
+
+            def worker(k):
+                b = bufs[k][1]
+                for i in range(reps + 10):
+                    if i == 0:
+                        gate.wait()
+                    t0 = time.perf_counter_ns()
+                    icrc_amd.compute_icrc_batch(b, off, lens, write_trailer=True)
+                    ok = icrc_amd.verify_icrc_batch(b, off, lens, zero_trailer=True)
+                    t1 = time.perf_counter_ns()
+                    if i >= 10:  # warm
+                        lat[k].append((t1 - t0) / 1e3)
+                    bad[k] += int(np.count_nonzero(ok != 1))
+
+            ths = [threading.Thread(target=worker, args=(k,)) for k in range(nth)]
+            t0 = time.perf_counter()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            secs = time.perf_counter() - t0
+            allv = np.concatenate([np.asarray(x) for x in lat])
+            out[f"c0_message_{kind}_{nth}_thread"] = {
+                "p50_us": round(float(np.percentile(allv, 50)), 1), "p99_us": round(float(np.percentile(allv, 99)), 1),
+                "messages_per_s": round(nth * (reps + 10) / secs, 1),
+                "GiB/s": round(nth * (reps + 10) * nbytes / secs / GIB, 3),
+                "failed_verifies": int(sum(bad)), "packets_per_message": int(w.n), "message_bytes": nbytes}
+    out["c0_message_note"] = ("per message: icrc_compute_batch(write_trailer=1) + icrc_verify_batch(zero_trailer=1) on "
+                              "a 64 x 4156-B WRITE in host memory; compare cpu_context.c0_roundtrip_1_core")
+    return out
+
+
 # ---- CPU stub (tests): the N>1 plumbing without GPUs -------------------------------------------
 def run_cpu_stub(args, rank: int, world: int) -> int:
     import zlib
@@ -625,6 +737,7 @@ def run_cpu_stub(args, rank: int, world: int) -> int:
         got[0] ^= 1
     fails = int(np.count_nonzero(got != want))
     agg = shard.aggregate(n * L * args.steps, wall, fails)
+    per_rank = shard.gather_floats([wall / args.steps * 1e3, rank, wall / args.steps * 1e3, 0.0])
     if rank == 0:
         print(json.dumps({
             "metric": METRIC + " [cpu-stub: plumbing test, not the ICRC]", "value": round(agg.gib_per_s, 6),
@@ -636,6 +749,7 @@ def run_cpu_stub(args, rank: int, world: int) -> int:
                        "packets_total_per_step": agg.total_bytes // args.steps // L,
                        "parallelism": f"shard-per-rank x{world} (gloo)"},
             "parity_sample": {"failures_all_ranks": agg.failures},
+            "per_rank": per_rank_fields(per_rank),
         }), flush=True)
     if world > 1:
         dist.barrier()

@@ -27,11 +27,14 @@
  *     ICRC_EINVAL.
  *   - The caller owns every buffer.  Synchronous calls retain no pointer; *_device calls
  *     borrow their pointers until the stream they were issued on is synchronised.
- *   - All entry points are reentrant.  Scalar calls copy the packet into a pinned staging slot of
- *     the calling thread and queue on the engine's combining submitter: concurrent callers are
- *     merged into one launch (one thread launches, the others wait for their results).  Host
- *     batches serialise per engine on its two pipelined staging buffers; device batches only
- *     enqueue on the caller's stream.  The default-engine registry is lock-protected.
+ *   - All entry points are reentrant.  Scalar calls, and host batches of at most 1024 packets and
+ *     8 MiB (one message: configs[0] is 64 x 4156 B), queue on the engine's combining submitter:
+ *     the kernel reads the packets from pinned, device-mapped host memory (the caller's own
+ *     buffer when it is pinned, else a copy in a staging slot of the calling thread), and
+ *     concurrent callers are merged into one launch (one thread launches, the others wait for
+ *     their results).  Larger host batches serialise per engine on its two pipelined H2D staging
+ *     buffers; device batches only enqueue on the caller's stream.  The default-engine registry
+ *     is lock-protected.
  *   - Every CRC is computed by the HIP kernel on the GPU; there is no CPU fallback.  With
  *     no usable GPU the calls return ICRC_ENODEV.
  */
@@ -74,15 +77,24 @@ int icrc_engine_default(int device, icrc_engine **out);
 int icrc_engine_device_ordinal(const icrc_engine *engine);
 /* The engine's own non-blocking stream (a hipStream_t), for callers without one. */
 void *icrc_engine_stream(const icrc_engine *engine);
-/* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode): 0 = one packet
- * per wavefront at a time; 13 / 16 = one packet per wavefront, software-pipelined, one / two CRC
- * chains per wave; 20 = four packets per wavefront; 24, 25, 26 = eight packets per wavefront;
- * 100 + q / 200 + q (q in 20, 24, 25, 26) = the default length-split dispatch with q as its
- * short-packet kernel (200: compacting long-packet walker); 301 = the fused single-pass receive
- * parse; -1 = the defaults (16 for uniform strided batches of long packets, 24 for short ones;
- * ragged batches are split by length between 24 and the long-packet kernel).  Results are
- * identical, except diagnostics 15, 18, 31, 32, 35 (ablations, wrong by design).
- * Other values: ICRC_EINVAL. */
+/* Tuning knob for A/B measurement (kernel variants, icrc_kernels.hip launch_mode).  Every value
+ * this library accepts gives identical results:
+ *   -1   the defaults: uniform strided batches of packets >= 1089 B and batches of at most one
+ *        packet per wave (#CUs x 16) take 16; strided batches of shorter packets take 40; larger
+ *        ragged batches are split by length in ONE launch (icrc_hybrid_kernel): 40 takes
+ *        L <= 1088, the long-packet kernel L >= 1089;
+ *   0    one packet per wavefront, not pipelined;
+ *   13 / 16 / 17  one packet per wavefront, software-pipelined, one / two CRC chains per wave
+ *        (17 = 16 without the raised wave priority around its load bursts);
+ *   40   eight packets per wavefront (the oct kernel, packets up to 1088 B; longer ones ride
+ *        along on its per-packet path);
+ *   140 / 240  the length split as two kernels forked / joined on two streams (240: the
+ *        compacting long-packet walker);
+ *   301 / 302  the receive parse as one fused pass on any batch (S = 2 / S = 1).
+ * Other values: ICRC_EINVAL.  The quad kernels (20, 24-26, 120-126, 220-226) and the diagnostics
+ * whose results are wrong by design (15, 18, 19, 21, 22, 31, 32, 35, 41-46, 141-146, 241-246)
+ * exist only in the A/B library libicrc_amd_ab.so (built with ICRC_AB_BUILD), which no product
+ * path loads. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
 int icrc_device_count(void);
@@ -281,6 +293,11 @@ typedef struct icrc_write_msg {
 /* Read requests: ack_req (the request is IbvSendSignaled, read.rs:37).  WRITE / READ RESPONSE
  * packets carry ack_req on their LAST / ONLY packet regardless (write.rs:41-90). */
 #define ICRC_WRITE_ACK_REQ 0x08u
+/* Emit the UDP payload only (BTH .. ICRC, L - 28 bytes) at each slot: the form
+ * generate_payload_from_msg returns and NetAgent::send_to takes (net/util.rs:183-185).  The ICRC
+ * is the same (it covers the masked IPv4 / UDP header, which is not stored); d_pkt_len reports
+ * L - 28, the bytes written. */
+#define ICRC_WRITE_UDP_PAYLOAD_ONLY 0x10u
 /* Number of packets generate_segments_from_request yields (common.rs:152-176) for a message
  * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_SEG_BY_REMOTE_VA);
  * 0 if pmtu == 0. */

@@ -36,29 +36,32 @@ struct Stage {
     uint32_t i0 = 0, cnt = 0;
 };
 
-// One scalar call (icrc_compute / icrc_verify) waiting for the combining submitter.
-struct ScalarReq {
-    const uint8_t *pkt;  // the caller's packet, already copied into its thread's pinned slot
-    uint32_t len;
-    int mode;
-    uint32_t result = 0;
+// One call waiting for the combining submitter: a scalar call (icrc_compute / icrc_verify, n = 1)
+// or a small host batch (one message's packets, icrc_compute_batch / icrc_verify_batch).  Always
+// an ICRC computation: verify compares with the trailer on the calling thread.
+struct SubmitReq {
+    const uint8_t *dbase;   // device view of the packets (a thread's mapped slot or the caller's pinned buffer)
+    const uint64_t *off;    // n offsets from dbase (host memory of the caller)
+    const uint32_t *len;    // n lengths
+    uint32_t n;
+    uint32_t *res;          // n ICRCs (host memory of the caller)
     int rc = ICRC_OK;
     bool done = false;
 };
 
-// The combining submitter: concurrent scalar calls (the emulator's send, packet-handler and
-// receive threads, packet_processor.rs:260 / udp_agent.rs:99) queue here; whichever caller finds no
-// launch in flight takes every queued call and runs them as ONE batch launch per mode (the others
-// wait on the condition variable), then hands out the results.  Packets are read by the kernel
-// straight from the callers' pinned, device-mapped staging slots (no copy engine); results come
-// back through mapped pinned memory.
+// The combining submitter: concurrent calls (the emulator's send, packet-handler and receive
+// threads, packet_processor.rs:260 / udp_agent.rs:99) queue here; whichever caller finds no launch
+// in flight takes the queued calls (up to kCap packets) and runs them as ONE compute launch (the
+// others wait on the condition variable), then hands out the results.  Packets are read by the
+// kernel straight from pinned, device-mapped host memory (no copy engine); results come back
+// through mapped pinned memory.
 struct Combiner {
     std::mutex mu;
     std::condition_variable cv;
-    std::vector<ScalarReq *> pending;
+    std::vector<SubmitReq *> pending;
     bool busy = false;
     hipStream_t stream = nullptr;
-    static constexpr uint32_t kCap = 256;  // calls per launch
+    static constexpr uint32_t kCap = 4096;  // packets per launch (#CUs x 16: one per wave)
     uint64_t *h_off = nullptr;             // pinned + mapped: packet offsets from the batch base
     uint32_t *h_len = nullptr;
     uint32_t *h_res = nullptr;
@@ -283,6 +286,9 @@ int finish_stage(icrc_engine *e, Stage &s, const HostJob &j) {
     return ICRC_OK;
 }
 
+int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n,
+                  uint32_t *out_icrc, uint8_t *ok, int trailer);
+
 int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, const uint32_t *len,
                uint32_t n, uint32_t *out_icrc, uint8_t *ok, int trailer) {
     if (!e) return ICRC_EINVAL;
@@ -291,6 +297,8 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
     int vrc = validate_host(base, off, len, n);
     if (vrc) return vrc;
     if (n == 0) return ICRC_OK;
+    const int mrc = message_batch(e, mode, base, off, len, n, out_icrc, ok, trailer);
+    if (mrc != 1) return mrc;
     DeviceGuard g(e->device);
     if (!g.ok) return ICRC_ENODEV;
     std::lock_guard<std::mutex> lk(e->mu);
@@ -395,26 +403,34 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     return dispatch(e, mode, p, stream);
 }
 
-// ---- scalar drop-ins -------------------------------------------------------------------------
-// Per-thread pinned, device-mapped staging: each calling thread copies its packet into a slot of its
-// own (no lock around the copy); the slot outlives the call, one per (thread, engine).
-struct ScalarSlot {
+// ---- scalar drop-ins and one-message host batches -------------------------------------------
+// Per-thread pinned, device-mapped staging: each calling thread copies its packets into a slot of
+// its own (no lock around the copy); the slot outlives the call, one per (thread, engine), and
+// grows to the largest call the thread has made.
+struct StageSlot {
     const icrc_engine *engine = nullptr;
     uint8_t *h = nullptr;  // pinned host
     uint8_t *d = nullptr;  // device view
-    ~ScalarSlot() {
+    size_t cap = 0;
+    ~StageSlot() {
         if (h) (void)hipHostFree(h);
     }
 };
 constexpr size_t kScalarSlotBytes = 65536 + 64;  // any packet the C-ABI accepts (len <= 65535)
-thread_local ScalarSlot t_slot;
+// Host batches up to this size take the submitter (zero-copy, one launch, combinable across
+// threads): one message of the emulator's (configs[0]: 64 x 4156 B) is far below it.  Larger
+// batches take the staged, pipelined H2D path (host_batch).
+constexpr uint32_t kMsgMaxPackets = 1024;
+constexpr size_t kMsgMaxBytes = size_t(8) << 20;
+thread_local StageSlot t_slot;
 
-int scalar_slot(const icrc_engine *e, uint8_t **h, uint8_t **d) {
-    if (t_slot.engine != e || !t_slot.h) {
+int stage_slot(const icrc_engine *e, size_t bytes, uint8_t **h, uint8_t **d) {
+    bytes = std::max(bytes, kScalarSlotBytes);
+    if (t_slot.engine != e || !t_slot.h || t_slot.cap < bytes) {
         if (t_slot.h) (void)hipHostFree(t_slot.h);
-        t_slot = ScalarSlot{};
+        t_slot = StageSlot{};
         void *p = nullptr;
-        if (hipHostMalloc(&p, kScalarSlotBytes, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
+        if (hipHostMalloc(&p, bytes, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
         void *dp = nullptr;
         if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
             (void)hipHostFree(p);
@@ -423,10 +439,24 @@ int scalar_slot(const icrc_engine *e, uint8_t **h, uint8_t **d) {
         t_slot.engine = e;
         t_slot.h = static_cast<uint8_t *>(p);
         t_slot.d = static_cast<uint8_t *>(dp);
+        t_slot.cap = bytes;
     }
     *h = t_slot.h;
     *d = t_slot.d;
     return ICRC_OK;
+}
+
+void combiner_release(Combiner &c) {
+    if (c.stream) {
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipStreamDestroy(c.stream);
+        c.stream = nullptr;
+    }
+    for (void *p : {static_cast<void *>(c.h_off), static_cast<void *>(c.h_len), static_cast<void *>(c.h_res)})
+        if (p) (void)hipHostFree(p);
+    c.h_off = nullptr;
+    c.h_len = nullptr;
+    c.h_res = nullptr;
 }
 
 Combiner *combiner(icrc_engine *e, int *rc) {
@@ -434,78 +464,94 @@ Combiner *combiner(icrc_engine *e, int *rc) {
     if (e->comb) return e->comb.get();
     auto c = std::make_unique<Combiner>();
     *rc = ICRC_EDEVICE;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
     void *a = nullptr, *b = nullptr, *r = nullptr;
-    if (hipHostMalloc(&a, Combiner::kCap * 8, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc(&b, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc(&r, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) {
-        *rc = ICRC_ENOMEM;
-        return nullptr;
-    }
-    c->h_off = static_cast<uint64_t *>(a);
-    c->h_len = static_cast<uint32_t *>(b);
-    c->h_res = static_cast<uint32_t *>(r);
     void *da = nullptr, *db = nullptr, *dr = nullptr;
-    if (hipHostGetDevicePointer(&da, a, 0) != hipSuccess || hipHostGetDevicePointer(&db, b, 0) != hipSuccess ||
-        hipHostGetDevicePointer(&dr, r, 0) != hipSuccess)
-        return nullptr;
-    c->d_off = static_cast<uint64_t *>(da);
-    c->d_len = static_cast<uint32_t *>(db);
-    c->d_res = static_cast<uint32_t *>(dr);
-    *rc = ICRC_OK;
-    e->comb = std::move(c);
-    return e->comb.get();
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        c->stream = nullptr;
+    } else if (hipHostMalloc(&a, Combiner::kCap * 8, hipHostMallocMapped) != hipSuccess ||
+               (c->h_off = static_cast<uint64_t *>(a), false) ||
+               hipHostMalloc(&b, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess ||
+               (c->h_len = static_cast<uint32_t *>(b), false) ||
+               hipHostMalloc(&r, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) {
+        *rc = ICRC_ENOMEM;
+    } else {
+        c->h_res = static_cast<uint32_t *>(r);
+        if (hipHostGetDevicePointer(&da, a, 0) == hipSuccess && hipHostGetDevicePointer(&db, b, 0) == hipSuccess &&
+            hipHostGetDevicePointer(&dr, r, 0) == hipSuccess) {
+            c->d_off = static_cast<uint64_t *>(da);
+            c->d_len = static_cast<uint32_t *>(db);
+            c->d_res = static_cast<uint32_t *>(dr);
+            *rc = ICRC_OK;
+            e->comb = std::move(c);
+            return e->comb.get();
+        }
+    }
+    combiner_release(*c);  // a failed set-up leaves nothing behind; the next call retries
+    return nullptr;
 }
 
 void combiner_free(icrc_engine *e) {
     if (!e->comb) return;
-    Combiner &c = *e->comb;
-    if (c.stream) {
-        (void)hipStreamSynchronize(c.stream);
-        (void)hipStreamDestroy(c.stream);
-    }
-    for (void *p : {static_cast<void *>(c.h_off), static_cast<void *>(c.h_len), static_cast<void *>(c.h_res)})
-        if (p) (void)hipHostFree(p);
+    combiner_release(*e->comb);
     e->comb.reset();
 }
 
-// One launch per mode over the taken calls (leader only, outside the combiner lock).
-void run_scalar_batch(icrc_engine *e, Combiner &c, ScalarReq *const *reqs, uint32_t n) {
-    for (int mode : {icrc::kCompute, icrc::kVerify}) {
-        uint32_t k = 0;
-        uintptr_t lo = UINTPTR_MAX;
-        for (uint32_t i = 0; i < n; i++)
-            if (reqs[i]->mode == mode) lo = std::min(lo, reinterpret_cast<uintptr_t>(reqs[i]->pkt));
-        for (uint32_t i = 0; i < n; i++) {
-            if (reqs[i]->mode != mode) continue;
-            c.h_off[k] = reinterpret_cast<uintptr_t>(reqs[i]->pkt) - lo;
-            c.h_len[k] = reqs[i]->len;
-            k++;
+// One compute launch over the taken calls (leader only, outside the combiner lock).
+void run_combined(icrc_engine *e, Combiner &c, SubmitReq *const *reqs, uint32_t nreq) {
+    uintptr_t lo = UINTPTR_MAX;
+    for (uint32_t i = 0; i < nreq; i++) lo = std::min(lo, reinterpret_cast<uintptr_t>(reqs[i]->dbase));
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < nreq; i++) {
+        const uint64_t rel = reinterpret_cast<uintptr_t>(reqs[i]->dbase) - lo;
+        for (uint32_t q = 0; q < reqs[i]->n; q++, k++) {
+            c.h_off[k] = rel + reqs[i]->off[q];
+            c.h_len[k] = reqs[i]->len[q];
         }
-        if (k == 0) continue;
-        BatchParams p{};
-        p.base = reinterpret_cast<uint8_t *>(lo);
-        p.off = c.d_off;
-        p.len = c.d_len;
-        p.n = k;
-        p.table = e->d_table;
-        p.table_quad = e->d_table_quad;
-        p.table_oct = e->d_table_oct;
-        if (mode == icrc::kCompute) p.out = c.d_res;
-        else p.ok = reinterpret_cast<uint8_t *>(c.d_res);
-        int rc = dispatch(e, mode, p, c.stream);
-        if (rc == ICRC_OK && hipStreamSynchronize(c.stream) != hipSuccess) rc = ICRC_EDEVICE;
-        k = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            if (reqs[i]->mode != mode) continue;
-            reqs[i]->rc = rc;
-            reqs[i]->result = mode == icrc::kCompute ? c.h_res[k] : reinterpret_cast<const uint8_t *>(c.h_res)[k];
-            k++;
-        }
+    }
+    BatchParams p{};
+    p.base = reinterpret_cast<uint8_t *>(lo);
+    p.off = c.d_off;
+    p.len = c.d_len;
+    p.n = k;
+    p.table = e->d_table;
+    p.table_quad = e->d_table_quad;
+    p.table_oct = e->d_table_oct;
+    p.out = c.d_res;
+    int rc = dispatch(e, icrc::kCompute, p, c.stream);
+    if (rc == ICRC_OK && hipStreamSynchronize(c.stream) != hipSuccess) rc = ICRC_EDEVICE;
+    k = 0;
+    for (uint32_t i = 0; i < nreq; i++) {
+        reqs[i]->rc = rc;
+        std::memcpy(reqs[i]->res, c.h_res + k, reqs[i]->n * sizeof(uint32_t));
+        k += reqs[i]->n;
     }
 }
 
-int scalar_call(int mode, const uint8_t *pkt, size_t len, uint32_t *result) {
+int submit(icrc_engine *e, Combiner *c, SubmitReq &req) {
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->pending.push_back(&req);
+    while (!req.done) {
+        if (!c->busy) {  // become the leader: take queued calls up to kCap packets, launch, hand out results
+            c->busy = true;
+            uint32_t take = 0, pk = 0;
+            while (take < c->pending.size() && (take == 0 || pk + c->pending[take]->n <= Combiner::kCap))
+                pk += c->pending[take++]->n;
+            std::vector<SubmitReq *> batch(c->pending.begin(), c->pending.begin() + take);
+            c->pending.erase(c->pending.begin(), c->pending.begin() + take);
+            lk.unlock();
+            run_combined(e, *c, batch.data(), take);
+            lk.lock();
+            for (SubmitReq *r : batch) r->done = true;
+            c->busy = false;
+            c->cv.notify_all();
+        } else {
+            c->cv.wait(lk);
+        }
+    }
+    return req.rc;
+}
+
+int scalar_call(const uint8_t *pkt, size_t len, uint32_t *result) {
     icrc_engine *e = nullptr;
     int rc = icrc_engine_default(-1, &e);
     if (rc) return rc;
@@ -514,32 +560,87 @@ int scalar_call(int mode, const uint8_t *pkt, size_t len, uint32_t *result) {
     Combiner *c = combiner(e, &rc);
     if (!c) return rc;
     uint8_t *h = nullptr, *d = nullptr;
-    if ((rc = scalar_slot(e, &h, &d)) != ICRC_OK) return rc;
+    if ((rc = stage_slot(e, len, &h, &d)) != ICRC_OK) return rc;
     std::memcpy(h, pkt, len);
-    ScalarReq req;
-    req.pkt = d;
-    req.len = static_cast<uint32_t>(len);
-    req.mode = mode;
-    std::unique_lock<std::mutex> lk(c->mu);
-    c->pending.push_back(&req);
-    while (!req.done) {
-        if (!c->busy) {  // become the leader: take every queued call, launch, hand out results
-            c->busy = true;
-            const uint32_t n = static_cast<uint32_t>(std::min<size_t>(c->pending.size(), Combiner::kCap));
-            std::vector<ScalarReq *> batch(c->pending.begin(), c->pending.begin() + n);
-            c->pending.erase(c->pending.begin(), c->pending.begin() + n);
-            lk.unlock();
-            run_scalar_batch(e, *c, batch.data(), n);
-            lk.lock();
-            for (ScalarReq *r : batch) r->done = true;
-            c->busy = false;
-            c->cv.notify_all();
-        } else {
-            c->cv.wait(lk);
+    const uint64_t off0 = 0;
+    const uint32_t len32 = static_cast<uint32_t>(len);
+    SubmitReq req{d, &off0, &len32, 1, result};
+    return submit(e, c, req);
+}
+
+// Device view of [base + smin, base + smax) when the caller's buffer is pinned host memory
+// (hipHostMalloc / hipHostRegister) covering the whole span, else nullptr.
+const uint8_t *pinned_device_view(uint8_t *base, uint64_t smin, uint64_t smax) {
+    if (!host_pinned(base + smin) || !host_pinned(base + smax - 1)) return nullptr;
+    void *d0 = nullptr, *d1 = nullptr;
+    if (hipHostGetDevicePointer(&d0, base + smin, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d1, base + smax - 1, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (static_cast<uint8_t *>(d1) - static_cast<uint8_t *>(d0) != static_cast<ptrdiff_t>(smax - 1 - smin)) return nullptr;
+    return static_cast<const uint8_t *>(d0);
+}
+
+// A host batch of at most kMsgMaxPackets / kMsgMaxBytes (one message): ICRCs through the
+// submitter, zero-copy from a pinned caller buffer, else packed into this thread's mapped slot;
+// then trailers written (compute) or compared and zeroed (verify) on the calling thread.
+// Returns 1 when the batch is too large for this path (the caller takes host_batch).
+int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n,
+                  uint32_t *out_icrc, uint8_t *ok, int trailer) {
+    if (n > kMsgMaxPackets) return 1;
+    size_t packed = 0;
+    uint64_t smin = UINT64_MAX, smax = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        packed += (static_cast<size_t>(len[i]) + 3) & ~size_t(3);
+        smin = std::min<uint64_t>(smin, off[i]);
+        smax = std::max<uint64_t>(smax, off[i] + len[i]);
+    }
+    if (packed > kMsgMaxBytes) return 1;
+    DeviceGuard g(e->device);
+    if (!g.ok) return ICRC_ENODEV;
+    int rc = ICRC_OK;
+    Combiner *c = combiner(e, &rc);
+    if (!c) return rc;
+    thread_local std::vector<uint64_t> t_off;
+    thread_local std::vector<uint32_t> t_res;
+    t_off.resize(n);
+    t_res.resize(n);
+    const uint8_t *dbase = (smax - smin) <= packed + packed / 4 + 4096 ? pinned_device_view(base, smin, smax) : nullptr;
+    if (dbase) {
+        for (uint32_t i = 0; i < n; i++) t_off[i] = off[i] - smin;
+    } else {
+        uint8_t *h = nullptr, *d = nullptr;
+        if ((rc = stage_slot(e, packed, &h, &d)) != ICRC_OK) return rc;
+        size_t pos = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            std::memcpy(h + pos, base + off[i], len[i]);
+            t_off[i] = pos;
+            pos += (static_cast<size_t>(len[i]) + 3) & ~size_t(3);
+        }
+        dbase = d;
+    }
+    SubmitReq req{dbase, t_off.data(), len, n, t_res.data()};
+    if ((rc = submit(e, c, req)) != ICRC_OK) return rc;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t *t = base + off[i] + len[i] - 4;
+        const uint32_t crc = t_res[i];
+        if (mode == icrc::kCompute) {
+            if (out_icrc) out_icrc[i] = crc;
+            if (trailer) {  // PacketWriter::write stores the ICRC LE (packet_processor.rs:260-263)
+                t[0] = uint8_t(crc);
+                t[1] = uint8_t(crc >> 8);
+                t[2] = uint8_t(crc >> 16);
+                t[3] = uint8_t(crc >> 24);
+            }
+        } else {  // is_icrc_valid (packet_processor.rs:341-353)
+            const uint32_t stored = static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |
+                                    (static_cast<uint32_t>(t[2]) << 16) | (static_cast<uint32_t>(t[3]) << 24);
+            ok[i] = stored == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+            if (trailer) std::memset(t, 0, 4);
         }
     }
-    *result = req.result;
-    return req.rc;
+    return ICRC_OK;
 }
 
 }  // namespace
@@ -547,8 +648,15 @@ int scalar_call(int mode, const uint8_t *pkt, size_t len, uint32_t *result) {
 extern "C" {
 
 const char *icrc_version(void) {
-    return "icrc_amd 0.2 gfx950: wave-per-packet end-aligned column Horner, LDS M^64 byte tables "
-           "(32x bank-replicated) + per-lane M^(64-l) nibble tables, prefetch ring, coalesced results";
+#ifdef ICRC_AB_BUILD
+#define ICRC_BUILD_KIND " [A/B build: quad kernels + diagnostics]"
+#else
+#define ICRC_BUILD_KIND ""
+#endif
+    return "icrc_amd 0.3 gfx950: wave-per-packet end-aligned column Horner, LDS M^64 byte tables "
+           "(32x bank-replicated) + per-lane M^(64-l) nibble tables, prefetch ring, coalesced results"
+           ICRC_BUILD_KIND;
+#undef ICRC_BUILD_KIND
 }
 
 int icrc_device_count(void) {
@@ -577,14 +685,20 @@ int icrc_engine_create(int device, icrc_engine **out) {
         return ICRC_EDEVICE;
     }
     e->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
-    std::vector<uint32_t> img(icrc::kLdsWords), img_quad(icrc::kLdsWords), img_oct(icrc::kLdsWords);
+    std::vector<uint32_t> img(icrc::kLdsWords), img_oct(icrc::kLdsWords);
     icrc::build_table_image(img.data());
-    icrc::build_table_image_quad(img_quad.data());
     icrc::build_table_image_oct(img_oct.data());
+#ifdef ICRC_AB_BUILD  // the quad kernels' image (A/B library only)
+    std::vector<uint32_t> img_quad(icrc::kLdsWords);
+    icrc::build_table_image_quad(img_quad.data());
+    if (hipMalloc(&e->d_table_quad, icrc::kLdsBytes) != hipSuccess ||
+        hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess) {
+        icrc_engine_destroy(e);
+        return ICRC_EDEVICE;
+    }
+#endif
     if (hipMalloc(&e->d_table, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table, img.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc(&e->d_table_quad, icrc::kLdsBytes) != hipSuccess ||
-        hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_table_oct, icrc::kLdsBytes) != hipSuccess ||
         hipMemcpy(e->d_table_oct, img_oct.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -668,7 +782,7 @@ uint32_t icrc_compute(const uint8_t *pkt, size_t len, int *err) {
         return 0;
     }
     uint32_t out = 0;
-    *rc = scalar_call(icrc::kCompute, pkt, len, &out);
+    *rc = scalar_call(pkt, len, &out);
     return *rc == ICRC_OK ? out : 0;
 }
 
@@ -680,7 +794,7 @@ int icrc_verify(uint8_t *pkt, size_t len, int zero_trailer, int *ok) {
     // return one ok byte per packet through mapped host memory: sub-dword PCIe writes, measured
     // twice as slow from three threads.
     uint32_t crc = 0;
-    const int rc = scalar_call(icrc::kCompute, pkt, len, &crc);
+    const int rc = scalar_call(pkt, len, &crc);
     if (rc != ICRC_OK) return rc;
     const uint8_t *t = pkt + len - 4;
     const uint32_t stored = static_cast<uint32_t>(t[0]) | (static_cast<uint32_t>(t[1]) << 8) |

@@ -63,8 +63,12 @@ constexpr int kHybridVariantBase = 100;
 // receive parse (A/B against the two-pass default).
 constexpr int kHybridCompactBase = 200;
 constexpr int kRxVariantBase = 300;
-// Variants a batch can be forced to (icrc_engine_set_kernel_variant); 15, 18, 31, 32, 35, 41-46
-// are diagnostics whose results are wrong by design.
+// Variants a batch can be forced to (icrc_engine_set_kernel_variant).  The product library
+// accepts only result-exact ones: 0, 13, 16, 17 (one packet per wave) and 40 (oct).  The A/B
+// library (built with ICRC_AB_BUILD: _build/libicrc_amd_ab.so, for measurement scripts and the
+// bench's loads-only denominator) adds the quad kernels 20, 24-26 (icrc_quad.hip) and the
+// diagnostics 15, 18, 19, 21, 22, 31, 32, 35, 41-46, whose results are wrong by design.
+#ifdef ICRC_AB_BUILD
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 24: case 25: case 26: case 31: case 32: case 35:
@@ -75,6 +79,10 @@ inline bool is_batch_variant(int v) {
     }
 }
 inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 46); }
+#else
+inline bool is_batch_variant(int v) { return v == 0 || v == 13 || v == 16 || v == 17 || v == 40; }
+inline bool is_short_variant(int v) { return v == 40; }
+#endif
 
 enum Mode : int { kCompute = 0, kVerify = 1 };
 
@@ -89,7 +97,8 @@ int launch_rx(const BatchParams &p, int grid, void *stream);  // fused verify + 
 // Receive parse pass 2 (the default path): descriptors from the header words, icrc_ok read from
 // p.ok where the verify pass left it.
 int launch_rx_desc(const BatchParams &p, int num_cu, void *stream);
-// Quad / chunked oct kernels (icrc_quad.hip), variants 20, 24-26 (and diagnostics 31, 32, 35).
+// Quad / chunked oct kernels (icrc_quad.hip, A/B library only), variants 20, 24-26 (and
+// diagnostics 31, 32, 35).
 int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);
 // Fixed-frame oct kernel (icrc_oct.hip), variant 40: packets of at most oct_max_len() bytes.
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag = 0);

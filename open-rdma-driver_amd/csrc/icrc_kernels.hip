@@ -269,6 +269,7 @@ struct SendPlan {
     uint32_t plen;  // payload bytes
     uint32_t hw;    // header words: 14 (IPv4 + UDP + BTH + RETH) or 18 (+ secondary RETH)
     uint32_t L;     // wire length: 4 hw + plen + pad + 4
+    uint32_t skip;  // leading packet bytes not stored: 28 under ICRC_WRITE_UDP_PAYLOAD_ONLY, else 0
     int k0;         // stream word index of lane 0 in ring row 0 (rows aligned to kRows)
     uint32_t pk;    // packet index (0xFFFFFFFF: empty slot)
     bool fits;      // a message, a pmtu, payload inside d_src, slot inside d_wire, L <= 0xFFFF
@@ -277,7 +278,7 @@ struct SendPlan {
 
 __device__ __forceinline__ void plan_empty(SendPlan &g) {
     g.src = g.out = 0;
-    g.start = g.plen = g.L = 0;
+    g.start = g.plen = g.L = g.skip = 0;
     g.hw = 14;
     g.k0 = 0;
     g.pk = 0xFFFFFFFFu;
@@ -308,9 +309,13 @@ __device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const
     }
     const uint32_t pad = (4u - (g.plen & 3u)) & 3u;
     g.L = 4u * g.hw + g.plen + pad + 4u;
+    // UDP payload only (generate_payload_from_msg returns BTH .. ICRC, net/util.rs:183-185): the
+    // slot receives packet bytes [28, L); the ICRC still covers the (masked) IPv4 / UDP header.
+    g.skip = (msg_flags(m) & ICRC_WRITE_UDP_PAYLOAD_ONLY) ? 28u : 0u;
     g.out = msg_u64(m, kMOutOff) + static_cast<uint64_t>(s) * msg_u32(m, kMSlot);
     g.src = msg_u64(m, kMPayloadOff) + g.start;
-    g.fits = g.plen <= src_bytes && g.src <= src_bytes - g.plen && g.L <= wire_bytes && g.out <= wire_bytes - g.L &&
+    const uint32_t span = g.L - g.skip;  // bytes stored into the slot
+    g.fits = g.plen <= src_bytes && g.src <= src_bytes - g.plen && span <= wire_bytes && g.out <= wire_bytes - span &&
              g.L <= 0xFFFFu;  // IPv4 total length (PacketWriter::write: LengthTooLong, packet_processor.rs:226)
     const int N = 1 + static_cast<int>((g.L - 4u) >> 2);
     g.k0 = N - 64 * kRows;
@@ -513,8 +518,11 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
         const uint32_t mA = head_mask(g.k0 + static_cast<int>(lane) + 64 * j0);
         const uint32_t mB = head_mask(g.k0 + static_cast<int>(lane) + 64 * (j0 + 1));
         const uint32_t room = 4u * g.hw + g.plen;  // bytes before the pad
+        // the slot holds packet bytes [skip, L): base = slot - skip, words below skip are not stored
+        uint8_t *const pbase = wire + g.out - g.skip;
+        const int pw_lo = static_cast<int>(g.skip >> 2);
         const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
-            wire + g.out, 0, g.fast ? static_cast<int>(g.L - 4u) : 0, 0x00020000);
+            pbase, 0, g.fast ? static_cast<int>(g.L - 4u) : 0, 0x00020000);
         uint32_t acc = 0;
 #pragma unroll
         for (int j = 0; j < kRows; ++j) {
@@ -525,15 +533,15 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                 const int keep = static_cast<int>(room) - 4 * pw;
                 w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
-            __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= 0 ? 4 * pw : static_cast<int>(kSendOOR), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, 0);
             const uint32_t uu = w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u));
             acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
         }
         const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
         const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
-            wire + g.out, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
+            pbase, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
-        send_record(res, pkt_len, icrc_out, npk, g.pk, g.L, crc, g.fast, lane);
+        send_record(res, pkt_len, icrc_out, npk, g.pk, g.L - g.skip, crc, g.fast, lane);
     };
 
     constexpr int B = D + 1;
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                 continue;
             }
             const uint32_t hvec = header_lanes(sm, sg, lane);
-            uint8_t *out = wire + sg.out;
+            uint8_t *out = wire + sg.out - sg.skip;  // packet byte 0 (bytes below skip are not stored)
             const int N = 1 + static_cast<int>((sg.L - 4u) >> 2);
             const int R = (N + 63) >> 6;
             const int k0 = N - 64 * R;
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
             for (int r = 0; r < R; ++r) {
                 const int pw = k0 - 1 + static_cast<int>(lane) + 64 * r;
                 const uint32_t w = packet_word_bytes(hvec, src, src_bytes, sg, pw);
-                if (pw >= 0 && static_cast<uint32_t>(4 * pw) < sg.L - 4u) {
+                if (pw >= 0 && static_cast<uint32_t>(4 * pw) >= sg.skip && static_cast<uint32_t>(4 * pw) < sg.L - 4u) {
                     out[4 * pw] = static_cast<uint8_t>(w);
                     out[4 * pw + 1] = static_cast<uint8_t>(w >> 8);
                     out[4 * pw + 2] = static_cast<uint8_t>(w >> 16);
@@ -608,7 +616,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                 t[1] = static_cast<uint8_t>(crc >> 8);
                 t[2] = static_cast<uint8_t>(crc >> 16);
                 t[3] = static_cast<uint8_t>(crc >> 24);
-                if (pkt_len) pkt_len[pk] = sg.L;
+                if (pkt_len) pkt_len[pk] = sg.L - sg.skip;
                 if (icrc_out) icrc_out[pk] = crc;
             }
         }
@@ -771,10 +779,12 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     switch (p.variant) {
     case 0: ICRC_LAUNCH_T(0, 1, 0); break;
     case 13: ICRC_LAUNCH_T(1, 1, 2 << 2); break;              // S = 1, nt row loads
+    case 17: ICRC_LAUNCH_T(2, 1, (2 << 2) | kAblNoPrio); break;  // 16 without the raised priority (A/B)
+    case 40: (void)launch_oct(MODE, p, grid, s); break;
+#ifdef ICRC_AB_BUILD  // the A/B library only: quad kernels and diagnostics (wrong results by design)
     case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2), false); break;  // diagnostic: loads only, nt
     case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2), false); break;  // diagnostic: CRC only (same shape as 15)
     case 19: ICRC_LAUNCH(2, 1, 1 | (2 << 2), false); break;  // diagnostic: loads only of the default (16) ring
-    case 17: ICRC_LAUNCH_T(2, 1, (2 << 2) | kAblNoPrio); break;  // 16 without the raised priority (A/B)
     case 21: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoFinal, false); break;  // diagnostic: 16 without final products
     case 22: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoStore, false); break;  // diagnostic: 16 without result stores
     case 20:
@@ -784,13 +794,13 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 31:
     case 32:
     case 35: (void)launch_quad(MODE, p.variant, p, grid, s); break;
-    case 40: (void)launch_oct(MODE, p, grid, s); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products
     case 44: (void)launch_oct(MODE, p, grid, s, 4); break;  // diagnostic: control only
     case 45: (void)launch_oct(MODE, p, grid, s, 5); break;  // diagnostic: loads only, no stores
     case 46: (void)launch_oct(MODE, p, grid, s, 6); break;  // diagnostic: no per-frame stores
+#endif
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }
 }

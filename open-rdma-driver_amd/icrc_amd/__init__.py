@@ -24,6 +24,10 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ICRC_AMD_LIB: another build of the same library (A/B measurements of two builds in one run)
 LIB_PATH = os.environ.get("ICRC_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd.so")
+# The A/B library: the same sources built with ICRC_AB_BUILD (quad kernels + diagnostic variants
+# whose results are wrong by design).  Loaded only on request (ab_library()), never by the product
+# path.
+AB_LIB_PATH = os.environ.get("ICRC_AMD_AB_LIB") or os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd_ab.so")
 
 OK = 0
 EINVAL = -22
@@ -98,6 +102,7 @@ WRITE_MSG_DTYPE = np.dtype([
     ("kind", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("_pad", "u1"), ("lkey", "<u4"),
 ])
 WRITE_FILL_IPV4_CSUM, WRITE_SEG_BY_REMOTE_VA, WRITE_SOLICITED, WRITE_ACK_REQ = 0x01, 0x02, 0x04, 0x08
+WRITE_UDP_PAYLOAD_ONLY = 0x10  # BTH .. ICRC at each slot (generate_payload_from_msg's form)
 assert WRITE_MSG_DTYPE.itemsize == 88
 MSG_WRITE, MSG_READ_RESPONSE, MSG_READ_REQUEST = 0, 1, 2
 
@@ -120,12 +125,12 @@ ACK_UDP_PAYLOAD_ONLY = 0x1
 EMULATOR_SRC_IP = 0xC0A80002  # 192.168.0.2, hard-coded in send_write_message (common.rs:124)
 
 
-def _load() -> ctypes.CDLL:
-    if not os.path.exists(LIB_PATH):
+def _load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
         raise ImportError(
-            f"icrc_amd: native library {LIB_PATH} is missing — build it with "
+            f"icrc_amd: native library {path} is missing — build it with "
             "`make -C open-rdma-driver_amd` (or __graft_entry__.build()); there is no fallback")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, u32, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
     sig = {
         "icrc_engine_create": (i32, [i32, ctypes.POINTER(vp)]),
@@ -173,6 +178,16 @@ def _load() -> ctypes.CDLL:
 
 
 lib = _load()
+_ab_lib = None
+
+
+def ab_library() -> ctypes.CDLL:
+    """The A/B build (libicrc_amd_ab.so): for Engine(device, lib=ab_library()) in measurement
+    scripts and bench.py's loads-only denominator (variant 19).  Not a product path."""
+    global _ab_lib
+    if _ab_lib is None:
+        _ab_lib = _load(AB_LIB_PATH)
+    return _ab_lib
 
 
 def _check(rc: int, what: str) -> None:
@@ -335,20 +350,26 @@ class Engine:
     torch.cuda.current_stream().cuda_stream); 0/None = the HIP null stream (torch's default
     stream), engine.stream = the engine's own non-blocking stream."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lib: Optional[ctypes.CDLL] = None):
+        self._lib = lib or globals()["lib"]
         h = ctypes.c_void_p()
-        _check(lib.icrc_engine_create(device, ctypes.byref(h)), "icrc_engine_create")
+        _check(self._lib.icrc_engine_create(device, ctypes.byref(h)), "icrc_engine_create")
         self.handle = h
         self.device = device
-        self.stream = lib.icrc_engine_stream(h) or 0
+        self.stream = self._lib.icrc_engine_stream(h) or 0
+
+    @property
+    def ordinal(self) -> int:
+        """The HIP device the engine runs on (icrc_engine_device_ordinal)."""
+        return int(self._lib.icrc_engine_device_ordinal(self.handle))
 
     def set_variant(self, variant: int) -> None:
         """Kernel variant for A/B runs (0 = unpipelined, S >= 1 = S packets in flight/wave)."""
-        _check(lib.icrc_engine_set_kernel_variant(self.handle, variant), "set_kernel_variant")
+        _check(self._lib.icrc_engine_set_kernel_variant(self.handle, variant), "set_kernel_variant")
 
     def close(self) -> None:
         if self.handle:
-            lib.icrc_engine_destroy(self.handle)
+            self._lib.icrc_engine_destroy(self.handle)
             self.handle = None
 
     def __del__(self):
@@ -359,40 +380,40 @@ class Engine:
 
     def compute_strided(self, d_base: int, stride: int, length: int, n: int, d_out: int,
                         write_trailer: bool = False, stream: Optional[int] = None) -> None:
-        _check(lib.icrc_compute_strided_device(self.handle, d_base, stride, length, n, d_out,
+        _check(self._lib.icrc_compute_strided_device(self.handle, d_base, stride, length, n, d_out,
                                                1 if write_trailer else 0, stream or None),
                "icrc_compute_strided_device")
 
     def verify_strided(self, d_base: int, stride: int, length: int, n: int, d_ok: int,
                        zero_trailer: bool = False, stream: Optional[int] = None) -> None:
-        _check(lib.icrc_verify_strided_device(self.handle, d_base, stride, length, n, d_ok,
+        _check(self._lib.icrc_verify_strided_device(self.handle, d_base, stride, length, n, d_ok,
                                               1 if zero_trailer else 0, stream or None),
                "icrc_verify_strided_device")
 
     def compute_batch(self, d_base: int, d_off: int, d_len: int, n: int, d_out: int,
                       write_trailer: bool = False, d_nerr: int = 0,
                       stream: Optional[int] = None) -> None:
-        _check(lib.icrc_compute_batch_device(self.handle, d_base, d_off, d_len, n, d_out or None,
+        _check(self._lib.icrc_compute_batch_device(self.handle, d_base, d_off, d_len, n, d_out or None,
                                              1 if write_trailer else 0, d_nerr or None,
                                              stream or None), "icrc_compute_batch_device")
 
     def verify_batch(self, d_base: int, d_off: int, d_len: int, n: int, d_ok: int,
                      zero_trailer: bool = False, d_nerr: int = 0,
                      stream: Optional[int] = None) -> None:
-        _check(lib.icrc_verify_batch_device(self.handle, d_base, d_off, d_len, n, d_ok,
+        _check(self._lib.icrc_verify_batch_device(self.handle, d_base, d_off, d_len, n, d_ok,
                                             1 if zero_trailer else 0, d_nerr or None,
                                             stream or None), "icrc_verify_batch_device")
 
     def synth(self, d_base: int, d_desc: int, d_hdr: int, n: int,
               stream: Optional[int] = None) -> None:
-        _check(lib.icrc_synth_device(self.handle, d_base, d_desc, d_hdr, n, stream or None),
+        _check(self._lib.icrc_synth_device(self.handle, d_base, d_desc, d_hdr, n, stream or None),
                "icrc_synth_device")
 
     def compute_batch_host(self, base: np.ndarray, off, lens, write_trailer: bool = False):
         off = np.ascontiguousarray(off, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         out = np.zeros(off.size, dtype=np.uint32)
-        _check(lib.icrc_compute_batch_ex(self.handle, _u8(base, writable=write_trailer).ctypes.data, off.ctypes.data,
+        _check(self._lib.icrc_compute_batch_ex(self.handle, _u8(base, writable=write_trailer).ctypes.data, off.ctypes.data,
                                          lens.ctypes.data, off.size, out.ctypes.data,
                                          1 if write_trailer else 0), "icrc_compute_batch_ex")
         return out
@@ -401,20 +422,20 @@ class Engine:
                  zero_trailer: bool = False, d_nerr: int = 0, stride: int = 0, length: int = 0,
                  stream: Optional[int] = None) -> None:
         """Fused receive (icrc_rx_parse_device): verify + strip + parse into RX_DESC_DTYPE."""
-        _check(lib.icrc_rx_parse_device(self.handle, d_base, d_off or None, d_len or None, stride, length, n,
+        _check(self._lib.icrc_rx_parse_device(self.handle, d_base, d_off or None, d_len or None, stride, length, n,
                                         d_desc, d_ok or None, 1 if zero_trailer else 0, d_nerr or None,
                                         stream or None), "icrc_rx_parse_device")
 
     def ipv4_checksum(self, d_base: int, n: int, d_off: int = 0, stride: int = 0, d_csum: int = 0,
                       fill: bool = False, stream: Optional[int] = None) -> None:
         """Batched IPv4 header checksum (icrc_ipv4_checksum_device, responser.rs:321-338)."""
-        _check(lib.icrc_ipv4_checksum_device(self.handle, d_base, d_off or None, stride, n, d_csum or None,
+        _check(self._lib.icrc_ipv4_checksum_device(self.handle, d_base, d_off or None, stride, n, d_csum or None,
                                              1 if fill else 0, stream or None), "icrc_ipv4_checksum_device")
 
     def ack_from_rx(self, d_desc: int, d_ctx: int, n: int, d_out: int, out_stride: int = 48, d_out_len: int = 0,
                     udp_payload_only: bool = False, stream: Optional[int] = None) -> None:
         """Receive-side auto-ACK (icrc_ack_from_rx_device, generate_ack net/util.rs:134-170)."""
-        _check(lib.icrc_ack_from_rx_device(self.handle, d_desc, d_ctx, n, d_out, out_stride, d_out_len or None,
+        _check(self._lib.icrc_ack_from_rx_device(self.handle, d_desc, d_ctx, n, d_out, out_stride, d_out_len or None,
                                            ACK_UDP_PAYLOAD_ONLY if udp_payload_only else 0, stream or None),
                "icrc_ack_from_rx_device")
 
@@ -422,7 +443,7 @@ class Engine:
                   d_wire: int, wire_bytes: int, d_pkt_len: int = 0, d_icrc: int = 0,
                   stream: Optional[int] = None) -> None:
         """Fused send step (icrc_write_packetize_device): segment, serialise, copy, pad, ICRC."""
-        _check(lib.icrc_write_packetize_device(self.handle, d_src or None, src_bytes, d_msgs, nmsgs,
+        _check(self._lib.icrc_write_packetize_device(self.handle, d_src or None, src_bytes, d_msgs, nmsgs,
                                                npackets, d_wire, wire_bytes, d_pkt_len or None,
                                                d_icrc or None, stream or None),
                "icrc_write_packetize_device")

@@ -10,8 +10,9 @@ no shared state (blue-rdma-device/src/device_inner.rs:119-171).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
-from typing import NamedTuple
+from typing import NamedTuple, Optional
 
 
 def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
@@ -59,3 +60,96 @@ def aggregate(bytes_local: int, seconds_local: float, failures_local: int, group
     secs = float(t.item())
     total_bytes, fails = (int(x) for x in c.tolist())
     return Aggregate(total_bytes / secs / float(1 << 30), secs, fails, total_bytes)
+
+
+def gather_floats(values, group=None) -> list:
+    """Every rank's list of floats (same length on every rank), rank-ordered; [values] when not
+    distributed.  One all-gather of a small tensor, outside any timed region (per-rank kernel
+    times and device ordinals for the rank-0 line)."""
+    import torch
+    import torch.distributed as dist
+
+    vals = [float(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized()):
+        return [vals]
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [o.cpu().tolist() for o in out]
+
+
+# ---- GPU count for the launcher, without initialising HIP in the launching process ----------
+_VISIBILITY_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def _visible_limit(env) -> Optional[int]:
+    """How many devices the visibility variables leave (None = unrestricted).  HIP applies
+    ROCR_VISIBLE_DEVICES first, then HIP_ / CUDA_VISIBLE_DEVICES on what remains: each set
+    variable caps the count at its number of entries."""
+    limit = None
+    for var in _VISIBILITY_VARS:
+        v = env.get(var)
+        if v is None:
+            continue
+        n = len([x for x in v.split(",") if x.strip() != ""])
+        limit = n if limit is None else min(limit, n)
+    return limit
+
+
+def kfd_gpu_count(sysfs: str = "/sys/class/kfd/kfd/topology/nodes") -> Optional[int]:
+    """GPU agents in the KFD topology (nodes whose `simd_count` is nonzero; CPU nodes have 0).
+    None when the topology cannot be read."""
+    try:
+        nodes = os.listdir(sysfs)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(sysfs, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    return n
+
+
+def amdsmi_gpu_count() -> Optional[int]:
+    """GPUs amdsmi enumerates (through the kernel driver, not HIP).  None if amdsmi is absent or
+    fails to initialise."""
+    try:
+        import amdsmi
+    except Exception:
+        return None
+    try:
+        amdsmi.amdsmi_init()
+    except Exception:
+        return None
+    try:
+        return len(amdsmi.amdsmi_get_processor_handles())
+    except Exception:
+        return None
+    finally:
+        try:
+            amdsmi.amdsmi_shut_down()
+        except Exception:
+            pass
+
+
+def visible_gpu_count(env=None, sysfs: str = "/sys/class/kfd/kfd/topology/nodes") -> tuple[int, str]:
+    """(GPUs this process may use, how it was counted) — the KFD topology, else amdsmi, capped by
+    the visibility variables.  Never calls HIP: bench.py's launcher uses it before starting the
+    ranks, so the parent process does not initialise a GPU.  Raises RuntimeError when neither
+    source works (no silent fallback to a HIP call)."""
+    env = os.environ if env is None else env
+    n, how = kfd_gpu_count(sysfs), "kfd-topology"
+    if n is None:
+        n, how = amdsmi_gpu_count(), "amdsmi"
+    if n is None:
+        raise RuntimeError("cannot count GPUs without HIP: no KFD topology at %s and amdsmi unavailable" % sysfs)
+    lim = _visible_limit(env)
+    if lim is not None and lim < n:
+        n, how = lim, how + "+visible-devices"
+    return n, how

@@ -94,3 +94,31 @@ def make_packets(rng):
     pkts.append(base[:43].copy())                                                   # L < 44
     pkts.append(base[:44].copy())
     return pkts
+
+
+# ---- the reference's own receive-parse expectations (rust_driver/.../tests/test_packet.rs:16-185) ----
+def reference_cases():
+    """tests/golden/rx_reference_cases.json (made by tests/golden/make_rx_reference.py): four
+    IPv4 packets and the fields test_packet.rs asserts `to_rdma_message` decodes from them."""
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rx_reference_cases.json")
+    with open(path) as f:
+        cases = json.load(f)
+    return [(c["name"], np.frombuffer(bytes.fromhex(c["packet"]), np.uint8), c["expect"]) for c in cases]
+
+
+def check_reference_expect(d, expect: dict, name: str = "") -> None:
+    """One descriptor (oracle.RX_DESC_DTYPE / icrc_rx_desc) against a test_packet.rs case."""
+    assert int(d["status"]) == 0 and int(d["icrc_ok"]) == 1, name
+    fl = int(d["flags"])
+    assert bool(fl & 0x10) == (expect["kind"] == "acknowledge"), name   # Metadata::Acknowledge / General
+    assert bool(fl & 0x01) == bool(expect["solicited"]), name
+    assert bool(fl & 0x02) == bool(expect["ack_req"]), name
+    assert bool(fl & 0x04) == ("imm" in expect), name                    # header.imm is Some
+    assert bool(fl & 0x08) == ("sec_va" in expect), name                 # secondary_reth is Some
+    for k, v in expect.items():
+        if k in ("kind", "solicited", "ack_req"):
+            continue
+        assert int(d[k]) == int(v), (name, k, int(d[k]), v)

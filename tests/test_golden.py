@@ -57,3 +57,13 @@ def test_gpu_matches_golden(engine):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), G["icrc"])
     np.testing.assert_array_equal(d_ok.cpu().numpy(), G["verify_ok"])
+
+
+def test_oracle_rx_parse_pinned_by_reference_test_packet():
+    """The oracle's to_rdma_message restatement decodes the four header shapes of the reference's
+    rust_driver/src/device/software/tests/test_packet.rs:16-185 to the values those tests assert."""
+    import rx_cases
+
+    for name, pkt, expect in rx_cases.reference_cases():
+        d = oracle.rx_parse(pkt.copy(), [0], [pkt.size])[0]
+        rx_cases.check_reference_expect(d, expect, name)

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
+from conftest import AB_ONLY_VARIANTS, engine_for
 from golden_kats import KATS, KAT1, KAT1_ICRC
 
 torch = pytest.importorskip("torch")
@@ -87,9 +88,10 @@ def test_ragged_any_length_any_alignment(engine, seed):
 
 
 @pytest.mark.parametrize("variant", [0, 13, 16, 17, 20, 24, 25, 26, 40])
-def test_every_kernel_variant_is_bit_exact(engine, variant):
+def test_every_kernel_variant_is_bit_exact(engine, ab_engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
+    engine = engine_for(variant, engine, ab_engine)
     rng = np.random.default_rng(100 + variant)
     n = 1500
     lens = rng.choice([44, 48, 316, 1084, 4156, 4157, 5000, 9000], n).astype(np.uint32)
@@ -170,12 +172,13 @@ def _quad_block_mix(rng, nblocks=48):
 
 @pytest.mark.parametrize("variant", [-1, 20, 24, 25, 26, 40, 120, 124, 140, 224, 240])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
-def test_quad_block_transitions_compute_verify(engine, variant, n):
+def test_quad_block_transitions_compute_verify(engine, ab_engine, variant, n):
     """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
     one-packet pipeline for the rest, or at these sizes the one-packet pipeline alone; 124 / 120: the
     split forced, with oct / quad; 224: oct with the compacting long-packet walker) on contrasting 64-packet blocks: compute with trailer
     write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
     trailer zeroing."""
+    engine = engine_for(variant, engine, ab_engine)
     rng = np.random.default_rng((variant % 100 + 2) * 1000 + n)
     off, lens = _quad_block_mix(rng)
     off, lens = off[:n], lens[:n]
@@ -411,6 +414,70 @@ def test_host_batch_multi_chunk(engine, pinned):
     np.testing.assert_array_equal(host, buf)  # trailers written back == the oracle's packets
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_message_batches_three_threads(pinned):
+    """One-message host batches (at most 1024 packets / 8 MiB: the submitter path, zero-copy from
+    pinned buffers, combined across threads) from three threads at once, as the emulator's send,
+    packet-handler and receive threads would call them: configs[0]-shaped WRITE messages and ragged
+    misaligned batches, compute with write_trailer then verify with zero_trailer, one corrupted
+    packet per batch; plus 1024 / 1025-packet batches on both sides of the size switch."""
+    import threading
+
+    import icrc_amd
+
+    def buffer(a):
+        if not pinned:
+            return a.copy()
+        t = torch.empty(a.size, dtype=torch.uint8, pin_memory=True)
+        h = t.numpy()
+        h[:] = a
+        keep.append(t)
+        return h
+
+    keep, errors = [], []
+
+    def run(seed):
+        try:
+            rng = np.random.default_rng(seed)
+            for it in range(12):
+                if it % 3 == 0:
+                    ref, off, lens = oracle.synth_write(256 << 10, 4096, local_va=0x7F7E8EE00000 + it * 4,
+                                                        remote_va=0x7F7E8FC00000, rkey=3, dqpn=2 + seed, psn0=it,
+                                                        msn=0, dst_ip=0xC0A80003, payload_key=seed * 100 + it)
+                else:
+                    n = int(rng.integers(1, 300))
+                    lens = rng.integers(44, 9000, n).astype(np.uint32)
+                    off = np.zeros(n, np.uint64)
+                    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 5, n - 1).astype(np.uint64))
+                    ref = rng.integers(0, 256, int(off[-1] + lens[-1]) + 3, dtype=np.uint8)
+                want = oracle_icrcs(ref, off, lens)
+                host = buffer(ref)
+                got = icrc_amd.compute_icrc_batch(host, off, lens, write_trailer=True)
+                np.testing.assert_array_equal(got, want)
+                bad = int(rng.integers(0, len(lens)))
+                host[int(off[bad]) + 40 + int(rng.integers(0, int(lens[bad]) - 44))] ^= 0x40
+                ok = icrc_amd.verify_icrc_batch(host, off, lens, zero_trailer=True)
+                expect = np.ones(len(lens), np.uint8)
+                expect[bad] = 0
+                np.testing.assert_array_equal(ok, expect)
+                tr = (off + lens.astype(np.uint64) - 4).astype(np.int64)[:, None] + np.arange(4)
+                assert not host[tr].any()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errors, errors
+    for n in (1024, 1025):  # the largest submitter batch, and the staged path
+        ref, off, lens = oracle.synth_middle_stream(n, pmtu=1024)
+        host = buffer(ref)
+        got = icrc_amd.compute_icrc_batch(host, off, lens)
+        np.testing.assert_array_equal(got, oracle_icrcs(ref, off, lens))
+
+
 def test_packet_writer_matches_oracle():
     import icrc_amd
 
@@ -530,6 +597,34 @@ def test_packetize_matches_oracle(engine, layout):
     np.testing.assert_array_equal(gl, wl)
     np.testing.assert_array_equal(gi, wi)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_packetize_udp_payload_only(engine, aligned):
+    """ICRC_WRITE_UDP_PAYLOAD_ONLY: every slot holds the oracle's packet from byte 28 (BTH .. ICRC,
+    generate_payload_from_msg's return value, net/util.rs:183-185), pkt_len = L - 28, same ICRC;
+    word path and byte path (misaligned payloads)."""
+    import icrc_amd
+
+    rng = np.random.default_rng(41 if aligned else 42)
+    specs, src_bytes = _random_specs(rng, 40, aligned)
+    for s in specs:
+        s["flags"] = (s["flags"] & 0x0F) | icrc_amd.WRITE_UDP_PAYLOAD_ONLY
+    msgs = icrc_amd.write_messages(specs)
+    src = rng.integers(0, 256, src_bytes + 16, dtype=np.uint8)
+    wire_bytes = int(msgs["out_offset"][-1]) + int(msgs["npackets"][-1]) * int(msgs["slot_stride"][-1]) + 64
+    want, wl, wi = oracle.send_messages(src, msgs, wire_bytes)
+    got, gl, gi = run_packetize(engine, src, msgs, wire_bytes, fill=0xEE)
+    np.testing.assert_array_equal(gi, wi)
+    np.testing.assert_array_equal(gl, np.where(wl > 0, wl - 28, 0))
+    k = 0
+    for m in msgs:
+        for s in range(int(m["npackets"])):
+            o, L = int(m["out_offset"]) + s * int(m["slot_stride"]), int(wl[k])
+            if L:
+                np.testing.assert_array_equal(got[o: o + L - 28], want[o + 28: o + L])
+                assert np.all(got[o + L - 28: o + int(m["slot_stride"])][:28] == 0xEE)
+            k += 1
 
 
 def test_packetize_reference_write_path(engine):
@@ -892,10 +987,11 @@ def test_empty_batches_are_noops(engine):
 
 @pytest.mark.parametrize("variant", [-1, 120, 124, 140])
 @pytest.mark.parametrize("pmtu", [256, 1024])
-def test_short_strided_stream_quad_path(engine, pmtu, variant):
+def test_short_strided_stream_quad_path(engine, ab_engine, pmtu, variant):
     """Uniform strided batches of short packets (at this size the one-packet pipeline by default;
     forced to the quad (120) or oct (124) kernel, non-ragged variant): compute, trailer write and
     verify against the oracle."""
+    engine = engine_for(variant, engine, ab_engine)
     n = 2000 + pmtu // 256  # not a multiple of 4 or 64
     buf, off, lens = oracle.synth_middle_stream(n, pmtu=pmtu)
     L = int(lens[0])
@@ -923,9 +1019,10 @@ def test_short_strided_stream_quad_path(engine, pmtu, variant):
 
 @pytest.mark.parametrize("variant", [-1, 124, 140])
 @pytest.mark.parametrize("n", [1, 2, 3, 5])
-def test_tiny_batches_every_path(engine, n, variant):
+def test_tiny_batches_every_path(engine, ab_engine, n, variant):
     """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block;
     the default (one-packet pipeline at this size) and the split forced (124)."""
+    engine = engine_for(variant, engine, ab_engine)
     rng = np.random.default_rng(900 + n)
     lens = rng.choice([44, 316, 1084, 4156, 9000], n).astype(np.uint32)
     off = np.zeros(n, np.uint64)
@@ -1020,16 +1117,25 @@ def test_split_batches_concurrent_streams(engine):
     assert not errors, errors
 
 
-def test_kernel_variant_validation(engine):
+DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 141, 146, 241)
+
+
+def test_kernel_variant_validation(engine, ab_engine):
+    """The product library accepts only result-exact variants; the diagnostics (wrong results by
+    design) and the quad kernels exist only in the A/B library (libicrc_amd_ab.so)."""
     import icrc_amd
 
-    for v in (-1, 0, 13, 15, 16, 17, 18, 19, 20, 21, 22, 24, 25, 26, 31, 32, 35, 40, 41, 42, 43, 44, 45, 46, 120, 124, 140, 146, 224, 240, 301, 302):
+    for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302):
         engine.set_variant(v)
     engine.set_variant(-1)
-    for v in (-2, 1, 10, 14, 23, 27, 36, 47, 99, 100, 116, 147, 303, 400):
+    for v in (-2, 1, 10, 14, 23, 27, 36, 47, 99, 100, 116, 147, 303, 400) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
         with pytest.raises(icrc_amd.IcrcError) as e:
             engine.set_variant(v)
-        assert e.value.rc == icrc_amd.EINVAL
+        assert e.value.rc == icrc_amd.EINVAL, v
+    for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
+        ab_engine.set_variant(v)
+    ab_engine.set_variant(-1)
+    assert "A/B build" in icrc_amd.ab_library().icrc_version().decode() and "A/B" not in icrc_amd.version()
 
 
 def test_scalar_surface_accepts_any_writable_buffer():

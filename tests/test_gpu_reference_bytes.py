@@ -291,3 +291,113 @@ def test_receive_then_ack_pipeline(engine):
         if k in want_acks:
             pkt, _ = oracle.generate_ack(int(m["msn"]), 500 + i, int(ctx[k]["expected_psn"]))
             np.testing.assert_array_equal(out[k], pkt)
+
+
+# ---- receive parse pinned to the reference's own decode expectations --------------------------
+def _rx_run(engine, buf, off, lens):
+    import icrc_amd
+
+    n = len(lens)
+    d_buf, d_off, d_len = dev(buf), dev(np.asarray(off, np.uint64)), dev(np.asarray(lens, np.uint32))
+    d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(), d_ok.data_ptr(),
+                    stream=stream_handle())
+    torch.cuda.synchronize()
+    return d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE), d_ok.cpu().numpy()
+
+
+@pytest.mark.parametrize("path", ["default_small", "two_pass", "fused_301", "fused_302", "default_large"])
+def test_rx_parse_reference_test_packet_cases(engine, path):
+    """rust_driver/src/device/software/tests/test_packet.rs:16-185 — BTH+RETH (WRITE_FIRST,
+    solicited, pkey 0x1234, va 1, rkey 0x12345678, len 1, 512-byte payload), BTH+RETH+Imm,
+    BTH+RETH+RETH (READ_REQUEST), BTH+AETH (msn 0x123456, code 2, value 5) — as IPv4 datagrams
+    with their ICRC, through every receive path: the small-batch fused pass (default), the two
+    passes (variant 16), the forced fused kernels (301, 302), and the default two-pass path of a
+    batch above #CUs x 16 packets (the cases repeated, packed at 4-byte-aligned offsets)."""
+    import rx_cases
+
+    cases = rx_cases.reference_cases()
+    reps = 1
+    if path == "default_large":
+        reps = torch.cuda.get_device_properties(0).multi_processor_count * 16 // len(cases) + 7
+    pkts = [p for _ in range(reps) for _, p, _ in cases]
+    lens = np.array([p.size for p in pkts], np.uint32)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum((lens[:-1].astype(np.uint64) + 3) // 4 * 4)
+    buf = np.zeros(int(off[-1]) + int(lens[-1]) + 8, np.uint8)
+    for o, p in zip(off, pkts):
+        buf[int(o): int(o) + p.size] = p
+    variant = {"two_pass": 16, "fused_301": 301, "fused_302": 302}.get(path, -1)
+    engine.set_variant(variant)
+    try:
+        desc, ok = _rx_run(engine, buf, off, lens)
+    finally:
+        engine.set_variant(-1)
+    assert np.all(ok == 1)
+    for i, d in enumerate(desc):
+        name, _, expect = cases[i % len(cases)]
+        rx_cases.check_reference_expect(d, expect, name)
+        assert int(d["payload_offset"]) == int(off[i]) + 28 + {0x06: 28, 0x09: 32, 0x0C: 44, 0x11: 16}[int(d["opcode"])]
+
+
+# ---- the packetizer on the reference's own segmentation case ----------------------------------
+@pytest.mark.parametrize("udp_only", [False, True])
+def test_packetizer_reference_6144_at_4096(engine, udp_only):
+    """queues/send/operations/common.rs:189-202 (generate_segments_from_request: 6144 bytes from
+    va 0x7F7E8EE00000 at PMTU 4096 -> [4096, 2048]) and the two packets :205-300 builds from it:
+    WRITE_FIRST psn 0 / WRITE_LAST psn 1 with ack_req, RETH va 0x7F7E8FC00000 then +4096, rkey
+    33554435, dqpn 2, pkey (msn) 0, 192.168.0.2 -> .3, payload byte i = i as u8.  The test's LAST
+    packet carries RETH len = last.len (2048); Write::handle -> send_write_message puts
+    common.total_len (6144) on every packet (common.rs:113), which is what the emulator sends and
+    what is asserted here (the captures that would decide the test are absent).
+    udp_only: the generate_payload_from_msg form the test compares (net/util.rs:183-185)."""
+    import icrc_amd
+    import rx_cases
+
+    va, rva, total, pmtu = 0x7F7E8EE00000, 0x7F7E8FC00000, 6144, 4096
+    src = (np.arange(total) & 0xFF).astype(np.uint8)
+    flags = icrc_amd.WRITE_UDP_PAYLOAD_ONLY if udp_only else 0
+    msgs = icrc_amd.write_messages([dict(local_va=va, remote_va=rva, payload_offset=0, total_len=total, pmtu=pmtu,
+                                         rkey=33554435, dqpn=2, psn=0, msn=0, dst_ip=0xC0A80003, kind=0,
+                                         flags=flags)], slot_stride=4224)
+    assert int(msgs["npackets"][0]) == 2
+    d_src, d_msgs = dev(src), dev(msgs.view(np.uint8))
+    d_wire = torch.full((2 * 4224,), 0xEE, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(2, dtype=torch.int32, device="cuda")
+    d_icrc = torch.zeros(2, dtype=torch.int32, device="cuda")
+    engine.packetize(d_src.data_ptr(), total, d_msgs.data_ptr(), 1, 2, d_wire.data_ptr(), 2 * 4224,
+                     d_len.data_ptr(), d_icrc.data_ptr(), stream=stream_handle())
+    torch.cuda.synchronize()
+    wire = d_wire.cpu().numpy()
+    skip = 28 if udp_only else 0
+    plens = [4096, 2048]
+    assert d_len.cpu().numpy().tolist() == [28 + 28 + p + 4 - skip for p in plens]
+    pkts = []
+    for s, plen in enumerate(plens):
+        L = 56 + plen + 4
+        got = wire[s * 4224: s * 4224 + L - skip]
+        assert np.all(wire[s * 4224 + L - skip: (s + 1) * 4224] == 0xEE)  # nothing past the packet
+        udp = got[28 - skip:]  # BTH .. ICRC
+        np.testing.assert_array_equal(udp[28: 28 + plen], src[4096 * s: 4096 * s + plen])
+        full = np.concatenate([np.zeros(28, np.uint8), udp]) if udp_only else got.copy()
+        if udp_only:  # rebuild the IPv4 / UDP header the ICRC covered (write_ip_udp_header)
+            full[:28] = np.frombuffer(bytes([0x45, 0, *L.to_bytes(2, "big"), 0, 1, 0, 0, 64, 17, 0, 0,
+                                             192, 168, 0, 2, 192, 168, 0, 3]) + (4791).to_bytes(2, "big") * 2
+                                      + (L - 20).to_bytes(2, "big") + b"\0\0", np.uint8)
+        assert int(full[-4:].view("<u4")[0]) == int(d_icrc.cpu().numpy().view(np.uint32)[s])
+        assert oracle.compute_icrc(full.tobytes()) == int(full[-4:].view("<u4")[0])
+        pkts.append(full)
+    # decode both packets with the product's receive parse: the fields the reference test sets
+    lens = np.array([p.size for p in pkts], np.uint32)
+    off = np.array([0, (int(lens[0]) + 3) & ~3], np.uint64)
+    buf = np.zeros(int(off[1]) + int(lens[1]), np.uint8)
+    for o, p in zip(off, pkts):
+        buf[int(o): int(o) + p.size] = p
+    desc, ok = _rx_run(engine, buf, off, lens)
+    assert ok.tolist() == [1, 1]
+    for s, (op, ack) in enumerate(((0x06, 0), (0x08, 1))):
+        rx_cases.check_reference_expect(desc[s], dict(kind="general", solicited=0, ack_req=ack, opcode=op, tran_type=0,
+                                                      psn=s, dqpn=2, pkey=0, reth_va=rva + 4096 * s,
+                                                      reth_rkey=33554435, reth_len=total, payload_len=plens[s]),
+                                        "common.rs:205-300 packet %d" % s)

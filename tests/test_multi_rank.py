@@ -120,6 +120,9 @@ def test_bench_launcher_world2_weak():
     assert res["config"]["bytes_total_per_step"] == 2 * 48 * STUB_L  # summed over both ranks
     assert res["config"]["packets_per_gpu"] == 48
     assert res["parity_sample"]["failures_all_ranks"] == 0
+    pr = res["per_rank"]  # every rank's own time and device, gathered outside the timed region
+    assert pr["device"] == [0, 1] and len(pr["kernel_ms"]) == 2 and len(pr["wall_ms_per_step"]) == 2
+    assert pr["kernel_ms_min"] == min(pr["kernel_ms"]) and pr["kernel_ms_max"] == max(pr["kernel_ms"])
 
 
 def test_bench_launcher_world2_strong():
@@ -145,3 +148,40 @@ def test_bench_single_rank_stub():
     rc, res, err = _bench("--packets", "8")
     assert rc == 0, err[-2000:]
     assert res["n_gpus"] == 1 and res["config"]["bytes_total_per_step"] == 8 * STUB_L
+
+
+def test_gpu_count_without_hip(tmp_path):
+    """bench.py's launcher counts GPUs from the KFD topology (GPU nodes: simd_count > 0), capped by
+    the visibility variables; it never calls HIP, and with no source at all it refuses loudly."""
+    from icrc_amd import shard
+
+    nodes = tmp_path / "nodes"
+    for i, simd in enumerate([0, 304, 304, 0, 304]):  # two CPU nodes, three GPU agents
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\ngfx_target_version 90500\n")
+    assert shard.visible_gpu_count({}, str(nodes)) == (3, "kfd-topology")
+    assert shard.visible_gpu_count({"HIP_VISIBLE_DEVICES": "1"}, str(nodes))[0] == 1
+    assert shard.visible_gpu_count({"ROCR_VISIBLE_DEVICES": "0,1", "HIP_VISIBLE_DEVICES": "0"}, str(nodes))[0] == 1
+    assert shard.visible_gpu_count({"CUDA_VISIBLE_DEVICES": "0,1,2,3,4,5"}, str(nodes))[0] == 3
+    if shard.amdsmi_gpu_count() is None:  # this container: no KFD, no amdsmi device
+        with pytest.raises(RuntimeError):
+            shard.visible_gpu_count({}, str(tmp_path / "absent"))
+
+
+def test_bench_launcher_refuses_without_gpu_count():
+    """Without --cpu-stub, --gpus 2 on a machine where neither the KFD topology nor amdsmi shows
+    two GPUs exits 2 before starting any rank."""
+    from icrc_amd import shard
+
+    try:
+        have, _ = shard.visible_gpu_count()
+    except RuntimeError:
+        have = 0
+    if have >= 2:
+        pytest.skip("this machine has 2 GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "torch.distributed.run" not in p.stderr
