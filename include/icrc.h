@@ -191,7 +191,9 @@ int icrc_rx_parse_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d
  * From the descriptors of icrc_rx_parse_device, the ACK every receive handler sends
  * (write_first.rs:35-82 and the ten other message handlers): needed when the packet parsed
  * (status ICRC_RX_OK), its ICRC verified (icrc_ok == ICRC_VERIFY_OK), it is not an ACK, ack_req
- * is set, its QP is valid (ctx.flags) and psn == ctx.expected_psn.  The ACK is generate_ack's
+ * is set, its QP is valid (ctx.flags QP_VALID), its memory-region check did not fail (ctx.flags
+ * MR_ERROR clear: copy_to_with_key, write_first.rs:35-44 — an abnormal packet is never
+ * auto-ACKed) and psn == ctx.expected_psn.  The ACK is generate_ack's
  * 48-byte packet: 192.168.0.3 -> 192.168.0.2, ip_id 1, UDP 4791 -> 4791, BTH {Acknowledge, RC,
  * pkey, dqpn = peer_qpn, psn = expected_psn}, AETH {Ack, 0x1f, msn = pkey} and its ICRC; with
  * ICRC_ACK_UDP_PAYLOAD_ONLY the 20-byte UDP payload generate_ack returns (util.rs:167-169).
@@ -200,9 +202,12 @@ int icrc_rx_parse_device(icrc_engine *engine, uint8_t *d_base, const uint64_t *d
 typedef struct icrc_ack_ctx {
     uint32_t peer_qpn;     /* qp_context.peer_qpn() of the packet's QP (dqpn)                */
     uint32_t expected_psn; /* qp_context.expected_psn() before this packet                    */
-    uint32_t flags;        /* ICRC_ACK_CTX_QP_VALID: the QP exists and is not in error state  */
+    uint32_t flags;        /* ICRC_ACK_CTX_* below                                            */
 } icrc_ack_ctx;
-#define ICRC_ACK_CTX_QP_VALID 0x1u
+#define ICRC_ACK_CTX_QP_VALID 0x1u /* the QP exists and is not in the error state (qp_error,
+                                      is_error(): write_first.rs:39-60)                          */
+#define ICRC_ACK_CTX_MR_ERROR 0x2u /* the packet's MR / key check failed (mr_error = copy_to_with_key
+                                      (msg).is_err(), write_first.rs:35): no ACK                 */
 #define ICRC_ACK_UDP_PAYLOAD_ONLY 0x1u
 int icrc_ack_from_rx_device(icrc_engine *engine, const icrc_rx_desc *d_desc, const icrc_ack_ctx *d_ctx, uint32_t n,
                             uint8_t *d_out, uint32_t out_stride, uint32_t *d_out_len, uint32_t flags,

@@ -627,7 +627,8 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
 // One thread per received packet.  The ACK is needed exactly when every receive handler would send
 // one (write_first.rs:35-82 and the ten other handlers): the packet parsed (status OK), its ICRC
 // verified, it is not itself an ACK, ack_req is set, the QP exists and is not in the error state,
-// and psn == the QP's expected PSN.  The 48-byte packet is generate_ack's PacketWriter output:
+// the packet's memory-region check passed (mr_error, write_first.rs:35-44), and psn == the QP's
+// expected PSN.  The 48-byte packet is generate_ack's PacketWriter output:
 // 192.168.0.3 -> 192.168.0.2, ip_id 1, ports 4791, BTH {Acknowledge, RC, pkey = the packet's
 // pkey, dqpn = peer_qpn, psn = expected_psn}, AETH {Ack, 0x1f, msn = pkey}, ICRC.  The ICRC of
 // these 44 bytes (+ the FF x 8 prefix, masked header) is computed byte-serially in the thread from
@@ -649,7 +650,8 @@ __global__ __launch_bounds__(256) void icrc_ack_kernel(const icrc_rx_desc *desc,
         const uint32_t icrc_ok = w17 & 0xFFu, status = (w17 >> 8) & 0xFFu;
         const icrc_ack_ctx x = ctx[i];
         const bool need = status == ICRC_RX_OK && icrc_ok == ICRC_VERIFY_OK && !(flags & ICRC_RX_ACKNOWLEDGE) &&
-                          (flags & ICRC_RX_ACK_REQ) && (x.flags & ICRC_ACK_CTX_QP_VALID) && psn == x.expected_psn;
+                          (flags & ICRC_RX_ACK_REQ) && (x.flags & ICRC_ACK_CTX_QP_VALID) &&
+                          !(x.flags & ICRC_ACK_CTX_MR_ERROR) && psn == x.expected_psn;
         if (out_len) out_len[i] = need ? ((mode & ICRC_ACK_UDP_PAYLOAD_ONLY) ? 20u : 48u) : 0u;
         if (!need) continue;
         uint32_t w[12];

@@ -483,6 +483,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     };
 
     int cycles = 0;
+    bool bailed = false;
     for (;;) {
         // top of the cycle: prepare the next block, then fetch the (offset, len) of the one after
         if (!nb_ready && nb_next < nblocks && (!RAGGED || mblk == nb_next)) {
@@ -521,8 +522,16 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         });
         if (ldone && inflight == 0) break;
         // Safety net: a block needs at most 32 frames (8 cycles of 2 P slots) plus a stall cycle;
-        // a bookkeeping bug must end in wrong results, never in waves that do not finish.
-        if (++cycles > 12 * nblocks + 16) break;
+        // a bookkeeping bug must end in flagged results, never in waves that do not finish.
+        if (++cycles > 12 * nblocks + 16) {
+            bailed = true;
+            break;
+        }
+    }
+    if (bailed) {  // never reached by correct bookkeeping: make it loud, not silent
+        for (uint32_t i = lane; i < nq; i += 64u) store_result<MODE>(p, lo + i, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN);
+        if (p.nerr && lane == 0) atomicAdd(p.nerr, nq);
+        return;
     }
 
     if (irregular) {  // L < 44, misaligned, L % 4 != 0, far-apart offsets: per packet

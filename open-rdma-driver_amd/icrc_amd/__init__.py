@@ -121,6 +121,7 @@ RX_SOLICITED, RX_ACK_REQ, RX_HAS_IMM, RX_HAS_SECONDARY_RETH, RX_ACKNOWLEDGE = 0x
 # icrc_ack_ctx (include/icrc.h): the QP state generate_ack reads (write_first.rs:35-82)
 ACK_CTX_DTYPE = np.dtype([("peer_qpn", "<u4"), ("expected_psn", "<u4"), ("flags", "<u4")])
 ACK_CTX_QP_VALID = 0x1
+ACK_CTX_MR_ERROR = 0x2  # the packet failed its MR / key check (write_first.rs:35): no ACK
 ACK_UDP_PAYLOAD_ONLY = 0x1
 EMULATOR_SRC_IP = 0xC0A80002  # 192.168.0.2, hard-coded in send_write_message (common.rs:124)
 

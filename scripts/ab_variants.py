@@ -27,7 +27,7 @@ def main():
     variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16,13,0").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
     launches = int(os.environ.get("LAUNCHES", "10"))
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     s = torch.cuda.current_stream().cuda_stream
     w1 = workloads.write_middle_stream(1 << 20)
     L = int(w1.lens[0])

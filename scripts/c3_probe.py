@@ -16,7 +16,7 @@ from icrc_amd import workloads  # noqa: E402
 
 
 def main():
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     s = torch.cuda.current_stream().cuda_stream
     w3 = workloads.write_message(16 << 20, 4096)
     b = workloads.synthesize(eng, w3, stream=s)

@@ -18,7 +18,7 @@ from icrc_amd import workloads  # noqa: E402
 
 
 def main():
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     s = torch.cuda.current_stream()
     for name, w in (("4096 x 4156 B", workloads.write_message(16 << 20, 4096)),
                     ("256 x 316 B", workloads.write_middle_stream(256, pmtu=256))):

@@ -38,7 +38,7 @@ def main():
     s = torch.cuda.current_stream()
     builds = []
     for v in [int(x) for x in sys.argv[2:]] or [-1]:
-        eng = icrc_amd.Engine(0)
+        eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
         eng.set_variant(v)
         builds.append((v, eng))
     alg = npk * (4096 + 4156 + 8)

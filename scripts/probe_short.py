@@ -17,7 +17,7 @@ from icrc_amd import workloads  # noqa: E402
 
 def main():
     variants = [int(v) for v in sys.argv[1].split(",")]
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     s = torch.cuda.current_stream().cuda_stream
     jobs = {}
     for pmtu in (256, 1024):

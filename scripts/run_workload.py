@@ -21,7 +21,7 @@ from icrc_amd import workloads  # noqa: E402
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "c2"
     launches = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     if len(sys.argv) > 3:
         eng.set_variant(int(sys.argv[3]))
     s = torch.cuda.current_stream().cuda_stream

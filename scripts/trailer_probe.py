@@ -29,7 +29,7 @@ def timed(fn, reps=20):
 
 
 def main():
-    eng = icrc_amd.Engine(0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
     s = torch.cuda.current_stream().cuda_stream
     n = 1 << 20
     w = workloads.write_middle_stream(n)

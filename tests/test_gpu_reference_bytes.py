@@ -168,14 +168,15 @@ def test_c3_full_size_roundtrip_with_negatives(engine):
 # ---- receive-side auto-ACK (icrc_ack_from_rx_device) vs generate_ack (net/util.rs:134-170) ----
 def _ack_expected(desc, ctx, udp_only=False):
     """The handlers' rule (write_first.rs:35-82): need_ack = can_auto_ack && ack_req, with
-    can_auto_ack = QP present && !error && psn == expected_psn; plus status OK / ICRC verified /
-    not itself an ACK.  The packet: the oracle's generate_ack restatement."""
+    can_auto_ack = !mr_error && QP present && !error && psn == expected_psn; plus status OK / ICRC
+    verified / not itself an ACK.  The packet: the oracle's generate_ack restatement."""
     import icrc_amd
 
     out, lens = {}, np.zeros(desc.size, np.uint32)
     for i, (d, x) in enumerate(zip(desc, ctx)):
         need = (d["status"] == icrc_amd.RX_OK and d["icrc_ok"] == 1 and not d["flags"] & icrc_amd.RX_ACKNOWLEDGE
-                and d["flags"] & icrc_amd.RX_ACK_REQ and x["flags"] & 1 and int(d["psn"]) == int(x["expected_psn"]))
+                and d["flags"] & icrc_amd.RX_ACK_REQ and x["flags"] & icrc_amd.ACK_CTX_QP_VALID
+                and not x["flags"] & icrc_amd.ACK_CTX_MR_ERROR and int(d["psn"]) == int(x["expected_psn"]))
         if need:
             pkt, udp = oracle.generate_ack(int(d["pkey"]), int(x["peer_qpn"]), int(x["expected_psn"]))
             out[i] = udp if udp_only else pkt
@@ -203,7 +204,8 @@ def test_ack_kernel_reproduces_kat3(engine):
 
 def test_ack_kernel_decision_and_bytes_vs_oracle(engine):
     """Random descriptors (every status, ICRC result, ACK / non-ACK opcodes, ack_req, QP valid or
-    not, PSN equal / unequal to the expected one): which packets get an ACK and its bytes."""
+    not, MR check failed or not, PSN equal / unequal to the expected one): which packets get an
+    ACK and its bytes."""
     import icrc_amd
 
     rng = np.random.default_rng(48)
@@ -217,7 +219,7 @@ def test_ack_kernel_decision_and_bytes_vs_oracle(engine):
     ctx = np.zeros(n, icrc_amd.ACK_CTX_DTYPE)
     ctx["peer_qpn"] = rng.integers(0, 1 << 32, n, dtype=np.uint64)
     ctx["expected_psn"] = np.where(rng.random(n) < 0.7, desc["psn"], rng.integers(0, 1 << 24, n))
-    ctx["flags"] = rng.choice([0, 1, 1, 1], n)
+    ctx["flags"] = rng.choice([0, 1, 1, 1, 1, 3, 2], n)  # QP_VALID, and MR_ERROR (mr_error, write_first.rs:35)
     for udp_only, stride in ((False, 48), (True, 20), (False, 64)):
         want, wlen = _ack_expected(desc, ctx, udp_only)
         assert 100 < len(want) < n  # ~4.5 % of the random descriptors qualify
