@@ -50,6 +50,7 @@ constexpr uint32_t kOctRelLimit = 0x7F000000u;  // packet offset in its block + 
 constexpr uint32_t kOctNotMine = 63u;           // sort key (>> 6) of a packet this kernel skips
 constexpr int kOctK = 10;                       // rows per frame (320 bytes of a packet)
 constexpr bool kOctPrio = true;
+constexpr bool kOctClampRows = true;            // a set's rows past its last one re-load that row
 constexpr int kOctPairs = 2;                    // ring positions of two frames: one pair in flight
 constexpr uint32_t kOctMaxL = 1088u;            // 34 rows, 4 frames: longer packets are the long kernel's
 
@@ -389,13 +390,20 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
 #pragma unroll
             for (int j = 0; j < K; ++j) S.u[j] = (o1 + 32u * j) * 0x9E3779B1u;
         } else {
-            // Rows past a packet's end read the bytes after it (bounded by the block's extent) and
-            // are never stepped: cheaper than a per-row descriptor select, and those bytes are the
-            // block's next packets (L2-resident).
+            // Rows past the set's last row (the tail frame of a set whose rows are not a multiple
+            // of K) are never stepped: they re-load the last real row instead of the bytes after
+            // the packet.  The row step rides in the scalar offset, clamped on the scalar unit
+            // (rrem is uniform), so the loads stay unconditional and the clamp costs no VALU;
+            // before, those rows fetched the next packets' lines again (C2 FETCH 1.21x the
+            // algorithmic bytes, the 1 KiB class 1.26x: profiles/r03_pmc_c2_fetch.txt).
+            const uint32_t rrem = fd >> 24;
+            const uint32_t cap = 32u * (rrem >= 2u ? rrem - 2u : 0u);
             S.u[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o0), 0, 0);
 #pragma unroll
-            for (int j = 1; j < K; ++j)
-                S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o1 + 32u * (j - 1)), 0, 0);
+            for (int j = 1; j < K; ++j) {
+                const uint32_t so = kOctClampRows ? (32u * (j - 1) < cap ? 32u * (j - 1) : cap) : 32u * (j - 1);
+                S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o1), static_cast<int>(so), 0);
+            }
             if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(0);
         }
         const bool last = (fd & kOctLast) != 0u;

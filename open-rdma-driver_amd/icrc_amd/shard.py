@@ -139,16 +139,18 @@ def amdsmi_gpu_count() -> Optional[int]:
 
 
 def visible_gpu_count(env=None, sysfs: str = "/sys/class/kfd/kfd/topology/nodes") -> tuple[int, str]:
-    """(GPUs this process may use, how it was counted) — the KFD topology, else amdsmi, capped by
-    the visibility variables.  Never calls HIP: bench.py's launcher uses it before starting the
+    """(GPUs this process may use, how it was counted) — the KFD topology and amdsmi (the smaller
+    count when both answer), capped by the visibility variables.  Never calls HIP: bench.py's launcher uses it before starting the
     ranks, so the parent process does not initialise a GPU.  Raises RuntimeError when neither
     source works (no silent fallback to a HIP call)."""
     env = os.environ if env is None else env
-    n, how = kfd_gpu_count(sysfs), "kfd-topology"
-    if n is None:
-        n, how = amdsmi_gpu_count(), "amdsmi"
-    if n is None:
+    found = [(c, name) for c, name in ((kfd_gpu_count(sysfs), "kfd-topology"), (amdsmi_gpu_count(), "amdsmi"))
+             if c is not None]
+    if not found:
         raise RuntimeError("cannot count GPUs without HIP: no KFD topology at %s and amdsmi unavailable" % sysfs)
+    # both sources when both answer: the smaller count (a container may see the host's topology
+    # nodes while only some GPUs are its own)
+    n, how = min(found)
     lim = _visible_limit(env)
     if lim is not None and lim < n:
         n, how = lim, how + "+visible-devices"

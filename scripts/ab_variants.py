@@ -27,23 +27,31 @@ def main():
     variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "16,13,0").split(",")]
     rounds = int(os.environ.get("ROUNDS", "5"))
     launches = int(os.environ.get("LAUNCHES", "10"))
-    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
+    # the product library (or ICRC_AMD_LIB's build) unless a variant exists only in the A/B build
+    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26) for v in variants if v >= 0)
+    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library() if ab_only else None)
     s = torch.cuda.current_stream().cuda_stream
-    w1 = workloads.write_middle_stream(1 << 20)
-    L = int(w1.lens[0])
-    b1 = workloads.synthesize(eng, w1, stream=s)
-    w2 = workloads.mixed_mtu_stream(4 << 20)
-    b2 = workloads.synthesize(eng, w2, stream=s)
-    o2, l2 = dev(w2.off), dev(w2.lens)
-    out1 = torch.zeros(w1.n, dtype=torch.int32, device="cuda")
-    out2 = torch.zeros(w2.n, dtype=torch.int32, device="cuda")
-    bytes1 = w1.n * L
-    bytes2 = int(w2.lens.astype(np.uint64).sum())
-    jobs = {
-        "C1": (lambda: eng.compute_strided(b1.data_ptr(), L, L, w1.n, out1.data_ptr(), False, s), bytes1, out1),
-        "C2": (lambda: eng.compute_batch(b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), w2.n, out2.data_ptr(),
-                                         False, 0, s), bytes2, out2),
-    }
+    jobs = {}
+    keep = []
+    for name in os.environ.get("JOBS", "C1,C2").split(","):
+        if name == "C1":
+            w1 = workloads.write_middle_stream(1 << 20)
+            L = int(w1.lens[0])
+            b1 = workloads.synthesize(eng, w1, stream=s)
+            out1 = torch.zeros(w1.n, dtype=torch.int32, device="cuda")
+            keep += [b1, out1]
+            jobs["C1"] = (lambda b1=b1, out1=out1, n=w1.n, L=L: eng.compute_strided(b1.data_ptr(), L, L, n, out1.data_ptr(),
+                                                                                   False, s), w1.n * L, out1)
+            continue
+        kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0)}[name]
+        w2 = workloads.mixed_mtu_stream(4 << 20, **kw)
+        b2 = workloads.synthesize(eng, w2, stream=s)
+        o2, l2 = dev(w2.off), dev(w2.lens)
+        out2 = torch.zeros(w2.n, dtype=torch.int32, device="cuda")
+        keep += [b2, o2, l2, out2]
+        jobs[name] = (lambda b2=b2, o2=o2, l2=l2, out2=out2, n=w2.n: eng.compute_batch(
+            b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), n, out2.data_ptr(), False, 0, s),
+            int(w2.lens.astype(np.uint64).sum()), out2)
     times = {(j, v): [] for j in jobs for v in variants}
     ref = {}
     for r in range(rounds):

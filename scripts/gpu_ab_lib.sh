@@ -11,7 +11,7 @@ B=${B_LIB:-open-rdma-driver_amd/_build_ab/libicrc_amd_old.so}
 for i in $(seq ${REPS:-3}); do
   for build in new old; do
     if [ $build = old ]; then export ICRC_AMD_LIB=$PWD/$B; else unset ICRC_AMD_LIB; fi
-    ROUNDS=3 timeout -k 10 300 python3 scripts/ab_variants.py ${VARIANTS:--1,19} > $OUT/ab_one.jsonl 2> $OUT/ab_one.err; rc=$?
+    ROUNDS=${ROUNDS:-3} timeout -k 10 300 python3 scripts/ab_variants.py ${VARIANTS:--1} > $OUT/ab_one.jsonl 2> $OUT/ab_one.err; rc=$?
     case $rc in 0) ;; *) echo "FATAL: ab_variants ($build) exited $rc"; tail -5 $OUT/ab_one.err; exit $rc;; esac
     sed "s/^{/{\"build\": \"$build\", \"rep\": $i, /" $OUT/ab_one.jsonl >> $OUT/ab_lib.jsonl
   done

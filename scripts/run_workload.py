@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Run one workload a few times with the default dispatch (for rocprofv3 --pmc / --stats).
 
-usage: run_workload.py {c1,c1w,c1vz,c2,c3,s316,packetize} [launches] [variant]
-  c1w: C1 compute with write_trailer; c1vz: C1 verify with zero_trailer; s316: 4 Mi strided
+usage: run_workload.py {c1,c1w,c1v,c1vz,c2,c2nr,c2s,c2k,c2m,c3,s316,packetize} [launches] [variant]
+  c2nr / c2s / c2k / c2m: C2 without ragged LAST packets / only the 256-B class / only the
+  1 KiB class / 256-B and 1 KiB classes (4 Mi packets each, packed, offset / length arrays);
+  c1w: C1 compute with write_trailer; c1v / c1vz: C1 verify without / with zero_trailer; s316: 4 Mi strided
   316-byte packets; packetize: the fused send packetizer over 192 x 16 MiB WRITE messages
   (786 K x 4156-B packets, as bench.py --extra)"""
 import os
@@ -25,13 +27,13 @@ def main():
     if len(sys.argv) > 3:
         eng.set_variant(int(sys.argv[3]))
     s = torch.cuda.current_stream().cuda_stream
-    if which in ("c1", "c1w", "c1vz", "s316"):
+    if which in ("c1", "c1w", "c1v", "c1vz", "s316"):
         w = workloads.write_middle_stream(1 << 22, pmtu=256) if which == "s316" else workloads.write_middle_stream(1 << 20)
         L = int(w.lens[0])
         b = workloads.synthesize(eng, w, stream=s)
         out = torch.zeros(w.n, dtype=torch.int32, device="cuda")
-        if which == "c1vz":
-            fn = lambda: eng.verify_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), True, s)  # noqa: E731
+        if which in ("c1v", "c1vz"):
+            fn = lambda: eng.verify_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), which == "c1vz", s)  # noqa: E731
         else:
             fn = lambda: eng.compute_strided(b.data_ptr(), L, L, w.n, out.data_ptr(), which == "c1w", s)  # noqa: E731
     elif which == "packetize":
@@ -49,7 +51,9 @@ def main():
         fn = lambda: eng.packetize(src.data_ptr(), src.numel(), dm.data_ptr(), nmsg, npk, wire.data_ptr(),  # noqa: E731
                                    wire.numel(), ln.data_ptr(), ic.data_ptr(), s)
     else:
-        w = workloads.mixed_mtu_stream(4 << 20) if which == "c2" else workloads.write_message(16 << 20, 4096)
+        kw = {"c2": {}, "c2nr": dict(ragged_frac=0.0), "c2s": dict(classes=(256,)), "c2k": dict(classes=(1024,)),
+              "c2m": dict(classes=(256, 1024))}
+        w = workloads.mixed_mtu_stream(4 << 20, **kw[which]) if which in kw else workloads.write_message(16 << 20, 4096)
         b = workloads.synthesize(eng, w, stream=s)
         o = torch.from_numpy(np.ascontiguousarray(w.off)).cuda()
         ln = torch.from_numpy(np.ascontiguousarray(w.lens)).cuda()

@@ -150,10 +150,13 @@ def test_bench_single_rank_stub():
     assert res["n_gpus"] == 1 and res["config"]["bytes_total_per_step"] == 8 * STUB_L
 
 
-def test_gpu_count_without_hip(tmp_path):
-    """bench.py's launcher counts GPUs from the KFD topology (GPU nodes: simd_count > 0), capped by
-    the visibility variables; it never calls HIP, and with no source at all it refuses loudly."""
+def test_gpu_count_without_hip(tmp_path, monkeypatch):
+    """bench.py's launcher counts GPUs from the KFD topology (GPU nodes: simd_count > 0) and amdsmi
+    (the smaller count), capped by the visibility variables; it never calls HIP, and with no
+    source at all it refuses loudly."""
     from icrc_amd import shard
+
+    monkeypatch.setattr(shard, "amdsmi_gpu_count", lambda: None)
 
     nodes = tmp_path / "nodes"
     for i, simd in enumerate([0, 304, 304, 0, 304]):  # two CPU nodes, three GPU agents
@@ -164,9 +167,10 @@ def test_gpu_count_without_hip(tmp_path):
     assert shard.visible_gpu_count({"HIP_VISIBLE_DEVICES": "1"}, str(nodes))[0] == 1
     assert shard.visible_gpu_count({"ROCR_VISIBLE_DEVICES": "0,1", "HIP_VISIBLE_DEVICES": "0"}, str(nodes))[0] == 1
     assert shard.visible_gpu_count({"CUDA_VISIBLE_DEVICES": "0,1,2,3,4,5"}, str(nodes))[0] == 3
-    if shard.amdsmi_gpu_count() is None:  # this container: no KFD, no amdsmi device
-        with pytest.raises(RuntimeError):
-            shard.visible_gpu_count({}, str(tmp_path / "absent"))
+    with pytest.raises(RuntimeError):
+        shard.visible_gpu_count({}, str(tmp_path / "absent"))
+    monkeypatch.setattr(shard, "amdsmi_gpu_count", lambda: 1)  # amdsmi sees fewer: it wins
+    assert shard.visible_gpu_count({}, str(nodes)) == (1, "amdsmi")
 
 
 def test_bench_launcher_refuses_without_gpu_count():
