@@ -130,6 +130,8 @@ int main() {
         run("8 pkts/wave, 32-B dword rows, default, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100>);
         run("8 pkts/wave, 32-B dword rows, default, +150 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 150>);
         run("8 pkts/wave, 32-B dword rows, default, +200 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 200>);
+        run("16 pkts/wave, 16-B dword rows, default, +50 VALU/set", 316, n316, short_rows<16, 0, 20, 0, 50>);
+        run("16 pkts/wave, 16-B dword rows, default, +100 VALU/set", 316, n316, short_rows<16, 0, 20, 0, 100>);
         run("1 pkt/wave, 256-B dword rows, default", 1084, n1084, short_rows<1, 0, 5, 0>);
         run("8 pkts/wave, 32-B dword rows, default", 1084, n1084, short_rows<8, 0, 34, 0>);
         run("16 pkts/wave, 16-B dword rows, default", 1084, n1084, short_rows<16, 0, 68, 0>);
