@@ -72,13 +72,13 @@ constexpr int kRxVariantBase = 300;
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 24: case 25: case 26: case 31: case 32: case 35:
-    case 40: case 41: case 42: case 43: case 44: case 45: case 46:
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48:
         return true;
     default:
         return false;
     }
 }
-inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 46); }
+inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 48); }
 #else
 inline bool is_batch_variant(int v) { return v == 0 || v == 13 || v == 16 || v == 17 || v == 40; }
 inline bool is_short_variant(int v) { return v == 40; }
@@ -108,7 +108,7 @@ uint32_t oct_max_len();
 int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);
 // The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
 // short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
-inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 6 ? oct_max_len() + 1u : kSplitLen; }
+inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 8 ? oct_max_len() + 1u : kSplitLen; }
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {

@@ -122,6 +122,9 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
 // (to_rdma_message, packet_processor.rs:18-71, as rx_store), and transposed back so the 64
 // descriptors (4608 contiguous bytes) leave as 18 coalesced dword stores.
 constexpr uint32_t kRxStride = 19;  // LDS words per packet row (odd: conflict-free lane = packet reads)
+constexpr uint32_t kRxWord0 = kRxW0, kRxHdrWords = kRxWords;    // header words the decode reads: 7..17 (icrc_long.h)
+constexpr uint32_t kRxGroups = 64u / kRxHdrWords;              // packets per load round (5)
+constexpr uint32_t kRxRounds = (64u + kRxGroups - 1u) / kRxGroups;  // 13
 
 __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
     __shared__ uint32_t sh_all[4 * 64 * kRxStride];
@@ -129,7 +132,9 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *sh = sh_all + wave * 64u * kRxStride;
     const uint32_t tw = gridDim.x * 4u;
-    const uint32_t g = lane / 18u, w = lane - 18u * g;  // header-load layout: packet group, word
+    // header-load layout: packet group g, word w of the BTH and its extensions (words 7..17,
+    // bytes 28..71: rx_decode reads nothing of the IPv4 / UDP header, so those lines are not fetched)
+    const uint32_t g = lane / kRxHdrWords, w = kRxWord0 + lane - kRxHdrWords * g;
     for (uint32_t base = (blockIdx.x * 4u + wave) * 64u; base < p.n; base += tw * 64u) {
         const uint32_t i = base + lane;
         const bool in = i < p.n;
@@ -149,35 +154,35 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
             const uint32_t dlo = static_cast<uint32_t>(__builtin_amdgcn_readlane(olo, f0));  // int: no sign extension
             const uint32_t dhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(ohi, f0));
             const uint8_t *dq = p.base + (static_cast<uint64_t>(dlo) | (static_cast<uint64_t>(dhi) << 32));
-            uint32_t hv[22];
+            uint32_t hv[kRxRounds];
 #pragma unroll
-            for (uint32_t r = 0; r < 22; ++r) {  // 3 packets per round, 66 >= 64
-                const uint32_t j = 3u * r + g;
+            for (uint32_t r = 0; r < kRxRounds; ++r) {  // kRxGroups packets per round
+                const uint32_t j = kRxGroups * r + g;
                 const int src = static_cast<int>((j & 63u) << 2);
                 const uint32_t jl = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lf)));
                 const uint32_t jlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(olo)));
                 const uint32_t jhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ohi)));
-                const bool k = g < 3u && j < 64u && 4u * w + 8u <= jl;  // jl = 0 for packets not on this path
+                const bool k = g < kRxGroups && j < 64u && 4u * w + 8u <= jl;  // jl = 0 for packets not on this path
                 const uint8_t *q =
                     k ? p.base + (static_cast<uint64_t>(jlo) | (static_cast<uint64_t>(jhi) << 32)) + 4u * w : dq;
                 hv[r] = *reinterpret_cast<const uint32_t *>(q);
             }
 #pragma unroll
-            for (uint32_t r = 0; r < 22; ++r) {
-                const uint32_t j = 3u * r + g;
-                if (g < 3u && j < 64u) sh[j * kRxStride + w] = hv[r];
+            for (uint32_t r = 0; r < kRxRounds; ++r) {
+                const uint32_t j = kRxGroups * r + g;
+                if (g < kRxGroups && j < 64u) sh[j * kRxStride + w] = hv[r];
             }
         }
         __builtin_amdgcn_wave_barrier();
         uint32_t h[18];
 #pragma unroll
-        for (uint32_t k = 0; k < 18; ++k) {  // words not loaded (dummy reads, short packets) read as 0
-            const uint32_t x = sh[lane * kRxStride + k];
+        for (uint32_t k = 0; k < 18; ++k) {  // words not loaded (dummy reads, short packets, 0..6) read as 0
+            const uint32_t x = k >= kRxWord0 ? sh[lane * kRxStride + k] : 0u;
             h[k] = (fast && 4u * k + 8u <= L) ? x : 0u;
         }
         if (!fast && L >= ICRC_MIN_PACKET) {  // misaligned or L % 4 != 0: byte-wise, this lane only
 #pragma unroll
-            for (uint32_t k = 0; k < 18; ++k) {
+            for (uint32_t k = kRxWord0; k < 18; ++k) {
                 uint32_t x = 0;
 #pragma unroll
                 for (uint32_t t = 0; t < 4; ++t) {
@@ -802,6 +807,8 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 44: (void)launch_oct(MODE, p, grid, s, 4); break;  // diagnostic: control only
     case 45: (void)launch_oct(MODE, p, grid, s, 5); break;  // diagnostic: loads only, no stores
     case 46: (void)launch_oct(MODE, p, grid, s, 6); break;  // diagnostic: no per-frame stores
+    case 47: (void)launch_oct(MODE, p, grid, s, 7); break;  // diagnostic: no final products
+    case 48: (void)launch_oct(MODE, p, grid, s, 8); break;  // diagnostic: set setup without bperm
 #endif
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }

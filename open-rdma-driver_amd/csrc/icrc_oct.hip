@@ -294,10 +294,12 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
     accB = xb;
 }
 
-// DIAG (ablation builds, variants 41-46): 1 = the loads without the row steps and final
+// DIAG (ablation builds, variants 41-48): 1 = the loads without the row steps and final
 // products, 2 = the row steps without the loads, 3 = neither loads nor row steps (control and
 // final products), 4 = control only, 5 = 1 without the per-frame stores, 6 = the full kernel
-// without the per-frame stores.
+// without the per-frame stores, 7 = the full kernel without the final products, 8 = the full
+// kernel with each set's per-lane packet data taken from the lane itself (no bperm before the
+// loads).
 template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
@@ -363,9 +365,11 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         const uint32_t set = fd & kFdSet;
         if (fd & kOctFirst) {  // set setup: this lane's packet is sorted position 8 set + grp
             const uint32_t ps = 8u * set + grp;
-            const uint32_t key = bperm(ps, LB.key);
-            const uint32_t vrel = bperm(ps, LB.vrel);
-            const uint32_t L = bperm(ps, LB.len);
+            // DIAG 8: this lane's own block entry instead of the set's (no LDS round trip on the
+            // path to the loads; wrong results by design)
+            const uint32_t key = DIAG == 8 ? LB.key : bperm(ps, LB.key);
+            const uint32_t vrel = DIAG == 8 ? LB.vrel : bperm(ps, LB.vrel);
+            const uint32_t L = DIAG == 8 ? LB.len : bperm(ps, LB.len);
             lreal = ps < static_cast<uint32_t>(__popcll(LB.mine));
             const uint32_t N = 1u + ((L - 4u) >> 2);
             const int z = static_cast<int>((8u - (N & 7u)) & 7u);
@@ -435,7 +439,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
     // around a store in the ring)
     auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
-        if constexpr (DIAG >= 5) return;
+        if constexpr (DIAG == 5 || DIAG == 6) return;
         if (TRAILER && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
@@ -464,7 +468,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         const uint32_t fa = SA.fl, fb = SB.fl;
         constexpr uint32_t kFast = kOctHave | kOctUni | kOctFull;
         uint32_t accA = acc_c, accB = 0;
-        if ((DIAG == 0 || DIAG == 2 || DIAG == 6) && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
+        if ((DIAG == 0 || DIAG == 2 || DIAG == 6 || DIAG == 7 || DIAG == 8) && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
             if (fa & kOctFirst) oct_rows2<true>(SA, SB, accA, accB, hm, lds, c);
             else oct_rows2<false>(SA, SB, accA, accB, hm, lds, c);
         } else {
@@ -474,12 +478,12 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         acc_c = (fb & kOctHave) ? accB : accA;
         uint32_t crcA = 0, crcB = 0;
         if (fa & fb & kOctLast) {  // both sets end here: the two final products interleave
-            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accA : final_mul(lds, accA, c.fin));
-            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accB : final_mul(lds, accB, c.fin));
+            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accA : final_mul(lds, accA, c.fin));
+            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accB : final_mul(lds, accB, c.fin));
         } else if (fa & kOctLast) {
-            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accA : final_mul(lds, accA, c.fin));
+            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accA : final_mul(lds, accA, c.fin));
         } else if (fb & kOctLast) {
-            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5) ? accB : final_mul(lds, accB, c.fin));
+            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accB : final_mul(lds, accB, c.fin));
         }
         inflight -= ((fa & kOctHave) ? 1 : 0) + ((fb & kOctHave) ? 1 : 0);
         // A's results (and its block's result store) before B's routing touches rbv: B may hold
@@ -630,7 +634,9 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
         case 3: ICRC_O(M, R, false, 3); break;                       \
         case 4: ICRC_O(M, R, false, 4); break;                       \
         case 5: ICRC_O(M, R, false, 5); break;                       \
-        default: ICRC_O(M, R, false, 6); break;                      \
+        case 6: ICRC_O(M, R, false, 6); break;                       \
+        case 7: ICRC_O(M, R, false, 7); break;                       \
+        default: ICRC_O(M, R, false, 8); break;                      \
         }                                                            \
     } while (0)
 #ifdef ICRC_AB_BUILD  // diagnostics 41-46 (wrong results by design): the A/B library only

@@ -22,7 +22,8 @@ from icrc_amd import workloads  # noqa: E402
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     variants = [int(v) for v in sys.argv[2:]] or [-1]
-    eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
+    # the product library (ICRC_AMD_LIB selects another build for a two-build A/B)
+    eng = icrc_amd.Engine(0)
     s = torch.cuda.current_stream().cuda_stream
     for name, w in (("786K x 4156 B", workloads.write_middle_stream(786432)),
                     ("4Mi x 316 B", workloads.write_middle_stream(1 << 22, pmtu=256))):

@@ -23,7 +23,9 @@ constexpr uint32_t kOOR = 0x80000000u;
 
 // P packets per wave (W = 64 / P lanes each), X4: 16 bytes per lane per row, R rows per packet
 // (row bytes RB = W * (X4 ? 16 : 4), R * RB >= L), AUX load policy (0 default, 2 nt).
-template <int P, int X4, int R, int AUX, int WORK = 0>
+// DEPTH: sets in flight while one is folded (3: two ahead, the default; 2: one ahead).  ST: a
+// 64-lane result store every 8 sets (what the oct kernel does once per 64-packet block).
+template <int P, int X4, int R, int AUX, int WORK = 0, int DEPTH = 3, int ST = 0>
 __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t L, uint32_t n, uint32_t *out) {
     constexpr int W = 64 / P;
     constexpr int B = X4 ? 16 : 4;
@@ -66,15 +68,36 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
 #pragma unroll
         for (int w = 0; w < WORK; ++w) acc = __builtin_amdgcn_perm(acc, acc + static_cast<uint32_t>(w), 0x05040302u + w);
     };
-    load(0, ua);
-    load(1, ub);
-    for (uint32_t t = 0; t < nsets; t += 3) {
-        load(t + 2, uc);
-        fold(ua);
-        load(t + 3, ua);
-        fold(ub);
-        load(t + 4, ub);
-        fold(uc);
+    const __amdgpu_buffer_rsrc_t rsout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(n * 4u), 0x00020000);
+    auto result = [&](uint32_t t) __attribute__((always_inline)) {  // after set t: every 8th set, one store
+        if constexpr (ST) {
+            if ((t & 7u) == 7u) __builtin_amdgcn_raw_buffer_store_b32(acc, rsout, (int)(4u * ((lo + t * P) & ~63u) + 4u * lane), 0, 0);
+        }
+    };
+    if constexpr (DEPTH == 3) {
+        load(0, ua);
+        load(1, ub);
+        for (uint32_t t = 0; t < nsets; t += 3) {
+            load(t + 2, uc);
+            fold(ua);
+            result(t);
+            load(t + 3, ua);
+            fold(ub);
+            result(t + 1);
+            load(t + 4, ub);
+            fold(uc);
+            result(t + 2);
+        }
+    } else {
+        load(0, ua);
+        for (uint32_t t = 0; t < nsets; t += 2) {
+            load(t + 1, ub);
+            fold(ua);
+            result(t);
+            load(t + 2, ua);
+            fold(ub);
+            result(t + 1);
+        }
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -103,7 +126,7 @@ int main() {
     uint32_t *out;
     const size_t cap = (size_t)1400 << 20;
     CK(hipMalloc(&d, cap));
-    CK(hipMalloc(&out, 4096));
+    CK(hipMalloc(&out, (size_t)4 << 22));
     CK(hipMemset(d, 0x5a, cap));
     const int reps = 20;
     auto run = [&](const char *name, uint32_t L, uint32_t n, auto kern) {
@@ -130,6 +153,11 @@ int main() {
         run("8 pkts/wave, 32-B dword rows, default, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100>);
         run("8 pkts/wave, 32-B dword rows, default, +150 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 150>);
         run("8 pkts/wave, 32-B dword rows, default, +200 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 200>);
+        run("8 pkts/wave, 32-B dword rows, default, depth 2", 316, n316, short_rows<8, 0, 10, 0, 0, 2>);
+        run("8 pkts/wave, 32-B dword rows, default, store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 1>);
+        run("8 pkts/wave, 32-B dword rows, default, depth 2, store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 2, 1>);
+        run("8 pkts/wave, 32-B dword rows, default, depth 2, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100, 2>);
+        run("8 pkts/wave, 32-B dword rows, default, depth 2, store / 8 sets, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100, 2, 1>);
         run("16 pkts/wave, 16-B dword rows, default, +50 VALU/set", 316, n316, short_rows<16, 0, 20, 0, 50>);
         run("16 pkts/wave, 16-B dword rows, default, +100 VALU/set", 316, n316, short_rows<16, 0, 20, 0, 100>);
         run("1 pkt/wave, 256-B dword rows, default", 1084, n1084, short_rows<1, 0, 5, 0>);
