@@ -122,7 +122,10 @@ int grid_for(const icrc_engine *e, uint32_t n);
 // long-packet workgroups take each CU as the oct ones retire; under a forced hybrid variant (A/B)
 // two kernels on the caller's stream and the engine's side stream, forked and joined by events.
 int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
-    const int grid = grid_for(e, p.n);
+    // spread (small host-mapped batches): one workgroup per packet up to #CUs, so that as many CUs
+    // as possible read host memory over PCIe at once
+    const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>(p.n, 1u), static_cast<uint32_t>(e->num_cu)))
+                              : grid_for(e, p.n);
     p.split_len = 0;
     if (e->variant >= 0 && e->variant < icrc::kHybridVariantBase) {
         p.variant = e->variant;
@@ -517,6 +520,7 @@ void run_combined(icrc_engine *e, Combiner &c, SubmitReq *const *reqs, uint32_t 
     p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
     p.out = c.d_res;
+    p.spread = k <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup ? 1 : 0;
     int rc = dispatch(e, icrc::kCompute, p, c.stream);
     if (rc == ICRC_OK && hipStreamSynchronize(c.stream) != hipSuccess) rc = ICRC_EDEVICE;
     k = 0;

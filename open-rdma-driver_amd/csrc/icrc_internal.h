@@ -49,6 +49,8 @@ struct BatchParams {
     uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
                          // long-packet kernel (launch_long) L >= split_len
     int long_variant;    // launch_long: 0 = filtered S = 2 pipeline (default), 1 = compacting S = 1 walker
+    int spread;          // one-packet pipeline: consecutive waves' packets on different workgroups
+                         // (small host-mapped batches: more CUs issue PCIe reads at once)
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)

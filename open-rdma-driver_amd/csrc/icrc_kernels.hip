@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     c.fin = kFinalBase + lane * 4u;
 
     const uint32_t tw = gridDim.x * kWavesPerGroup;
-    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    const uint32_t gw = p.spread ? wave * gridDim.x + blockIdx.x : blockIdx.x * kWavesPerGroup + wave;
     if constexpr (S == 0) {
         for (uint32_t i = gw; i < p.n; i += tw) {
             const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;

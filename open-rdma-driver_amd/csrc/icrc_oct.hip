@@ -401,7 +401,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             // before, those rows fetched the next packets' lines again (C2 FETCH 1.21x the
             // algorithmic bytes, the 1 KiB class 1.26x: profiles/r03_pmc_c2_fetch.txt).
             const uint32_t rrem = fd >> 24;
-            const uint32_t cap = 32u * (rrem >= 2u ? rrem - 2u : 0u);
+            const uint32_t cap = 32u * (rrem > 2u ? rrem : 2u) - 64u;  // rows 1..rrem-1 real (no select chain)
             S.u[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o0), 0, 0);
 #pragma unroll
             for (int j = 1; j < K; ++j) {

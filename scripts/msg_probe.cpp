@@ -1,0 +1,85 @@
+// scripts/msg_probe.cpp — latency of ONE message through the host-resident batch drop-ins, the
+// emulator's granularity for configs[0] (BASELINE.json: 1 QP, 64 x 4 KiB RDMA WRITE, ICRC compute
+// + verify): icrc_compute_batch(write_trailer = 1) on the send side (PacketWriter::write,
+// packet_processor.rs:260-263), icrc_verify_batch(zero_trailer = 1) on the receive side
+// (is_icrc_valid, packet_processor.rs:341-353).  Cases: pinned / pageable message buffers; 64
+// packets, and 1 packet (the per-call floor).  Run it under rocprofv3 --kernel-trace --stats to
+// split each call into kernel time and the rest.  Prints one JSON line per case (p50 / p99 /
+// mean microseconds per call); every verify must succeed.
+// Build: see scripts/Makefile (links libicrc_amd.so and the HIP runtime for pinned memory).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "icrc.h"
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+double pct(std::vector<double> v, double q) {
+    std::sort(v.begin(), v.end());
+    return v[static_cast<size_t>(q * (v.size() - 1))];
+}
+
+void run(const char *name, uint8_t *buf, uint32_t npk, uint32_t L, int calls) {
+    std::vector<uint64_t> off(npk);
+    std::vector<uint32_t> len(npk, L);
+    for (uint32_t i = 0; i < npk; ++i) off[i] = static_cast<uint64_t>(i) * L;
+    std::vector<uint32_t> crc(npk);
+    std::vector<uint8_t> ok(npk);
+    std::vector<double> tc, tv;
+    long bad = 0;
+    for (int c = 0; c < calls + 20; ++c) {
+        const auto t0 = clk::now();
+        const int r1 = icrc_compute_batch(buf, off.data(), len.data(), npk, crc.data(), 1);
+        const auto t1 = clk::now();
+        const int r2 = icrc_verify_batch(buf, off.data(), len.data(), npk, ok.data(), 1);
+        const auto t2 = clk::now();
+        if (r1 || r2) bad++;
+        for (uint32_t i = 0; i < npk; ++i) bad += ok[i] != ICRC_VERIFY_OK;
+        if (c >= 20) {
+            tc.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+            tv.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
+        }
+    }
+    double mc = 0, mv = 0;
+    for (double x : tc) mc += x;
+    for (double x : tv) mv += x;
+    printf("{\"case\": \"%s\", \"packets\": %u, \"packet_bytes\": %u, \"compute_p50_us\": %.1f, \"compute_p99_us\": %.1f, "
+           "\"compute_mean_us\": %.1f, \"verify_p50_us\": %.1f, \"verify_p99_us\": %.1f, \"verify_mean_us\": %.1f, "
+           "\"bad\": %ld}\n",
+           name, npk, L, pct(tc, 0.5), pct(tc, 0.99), mc / tc.size(), pct(tv, 0.5), pct(tv, 0.99), mv / tv.size(), bad);
+    fflush(stdout);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const int calls = argc > 1 ? atoi(argv[1]) : 2000;
+    const uint32_t L = 4156, npk = 64;
+    std::vector<uint8_t> pageable(static_cast<size_t>(npk) * L);
+    uint32_t x = 12345;
+    for (auto &b : pageable) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        b = static_cast<uint8_t>(x);
+    }
+    uint8_t *pinned = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void **>(&pinned), pageable.size(), hipHostMallocDefault) != hipSuccess) {
+        fprintf(stderr, "hipHostMalloc failed\n");
+        return 1;
+    }
+    std::memcpy(pinned, pageable.data(), pageable.size());
+    run("pinned", pinned, npk, L, calls);
+    run("pageable", pageable.data(), npk, L, calls);
+    run("pinned_1_packet", pinned, 1, L, calls);
+    run("pageable_1_packet", pageable.data(), 1, L, calls);
+    (void)hipHostFree(pinned);
+    return 0;
+}

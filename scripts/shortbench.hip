@@ -23,8 +23,10 @@ constexpr uint32_t kOOR = 0x80000000u;
 
 // P packets per wave (W = 64 / P lanes each), X4: 16 bytes per lane per row, R rows per packet
 // (row bytes RB = W * (X4 ? 16 : 4), R * RB >= L), AUX load policy (0 default, 2 nt).
-// DEPTH: sets in flight while one is folded (3: two ahead, the default; 2: one ahead).  ST: a
-// 64-lane result store every 8 sets (what the oct kernel does once per 64-packet block).
+// DEPTH: sets in flight while one is folded (3: two ahead, the default; 2: one ahead).  ST: result
+// stores (the oct kernel stores a block's 64 results once per 8 sets): 1 = one store every 8 sets
+// (uniform branch); 2 = a store every set, out of range except every 8th (no branch); 3 = four
+// stores every 32 sets (branch); 4 = as 1 with the nt policy; 5 = as 2 with the nt policy.
 template <int P, int X4, int R, int AUX, int WORK = 0, int DEPTH = 3, int ST = 0>
 __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t L, uint32_t n, uint32_t *out) {
     constexpr int W = 64 / P;
@@ -69,9 +71,17 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
         for (int w = 0; w < WORK; ++w) acc = __builtin_amdgcn_perm(acc, acc + static_cast<uint32_t>(w), 0x05040302u + w);
     };
     const __amdgpu_buffer_rsrc_t rsout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(n * 4u), 0x00020000);
-    auto result = [&](uint32_t t) __attribute__((always_inline)) {  // after set t: every 8th set, one store
-        if constexpr (ST) {
-            if ((t & 7u) == 7u) __builtin_amdgcn_raw_buffer_store_b32(acc, rsout, (int)(4u * ((lo + t * P) & ~63u) + 4u * lane), 0, 0);
+    auto result = [&](uint32_t t) __attribute__((always_inline)) {  // after set t
+        const int o = (int)(4u * ((lo + t * P) & ~63u) + 4u * lane);
+        if constexpr (ST == 1 || ST == 4) {
+            if ((t & 7u) == 7u) __builtin_amdgcn_raw_buffer_store_b32(acc, rsout, o, 0, ST == 4 ? 2 : 0);
+        } else if constexpr (ST == 2 || ST == 5) {
+            __builtin_amdgcn_raw_buffer_store_b32(acc, rsout, (t & 7u) == 7u ? o : (int)kOOR, 0, ST == 5 ? 2 : 0);
+        } else if constexpr (ST == 3) {
+            if ((t & 31u) == 31u) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(acc + k, rsout, o - 256 * 8 * k, 0, 0);
+            }
         }
     };
     if constexpr (DEPTH == 3) {
@@ -153,6 +163,10 @@ int main() {
         run("8 pkts/wave, 32-B dword rows, default, +100 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 100>);
         run("8 pkts/wave, 32-B dword rows, default, +150 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 150>);
         run("8 pkts/wave, 32-B dword rows, default, +200 VALU/set", 316, n316, short_rows<8, 0, 10, 0, 200>);
+        run("8 pkts/wave, 32-B dword rows, default, store every set (OOR but 1 in 8)", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 2>);
+        run("8 pkts/wave, 32-B dword rows, default, 4 stores / 32 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 3>);
+        run("8 pkts/wave, 32-B dword rows, default, nt store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 4>);
+        run("8 pkts/wave, 32-B dword rows, default, nt store every set (OOR but 1 in 8)", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 5>);
         run("8 pkts/wave, 32-B dword rows, default, depth 2", 316, n316, short_rows<8, 0, 10, 0, 0, 2>);
         run("8 pkts/wave, 32-B dword rows, default, store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 1>);
         run("8 pkts/wave, 32-B dword rows, default, depth 2, store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 2, 1>);
