@@ -43,7 +43,8 @@ def main():
             jobs["C1"] = (lambda b1=b1, out1=out1, n=w1.n, L=L: eng.compute_strided(b1.data_ptr(), L, L, n, out1.data_ptr(),
                                                                                    False, s), w1.n * L, out1)
             continue
-        kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0)}[name]
+        kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0),
+              "C2m": dict(classes=(256, 1024)), "C2snr": dict(classes=(256,), ragged_frac=0.0)}[name]
         w2 = workloads.mixed_mtu_stream(4 << 20, **kw)
         b2 = workloads.synthesize(eng, w2, stream=s)
         o2, l2 = dev(w2.off), dev(w2.lens)

@@ -26,7 +26,12 @@ constexpr uint32_t kOOR = 0x80000000u;
 // DEPTH: sets in flight while one is folded (3: two ahead, the default; 2: one ahead).  ST: result
 // stores (the oct kernel stores a block's 64 results once per 8 sets): 1 = one store every 8 sets
 // (uniform branch); 2 = a store every set, out of range except every 8th (no branch); 3 = four
-// stores every 32 sets (branch); 4 = as 1 with the nt policy; 5 = as 2 with the nt policy.
+// stores every 32 sets (branch); 4 = as 1 with the nt policy; 5 = as 2 with the nt policy;
+// 6 = results held in a 16-register shift buffer (one entry per 8 sets), stored as a burst of 16
+// when full and at the end; 7 = the same with a 4-register buffer (4 stores every 32 sets);
+// 8 = the 16-register buffer stored only after the loop (no store in the loop body; results
+// beyond 16 blocks per wave are dropped); 9 = the wave's chunk walked in passes of 16 blocks,
+// each pass's loop drained before its 16 results are stored.
 template <int P, int X4, int R, int AUX, int WORK = 0, int DEPTH = 3, int ST = 0>
 __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t L, uint32_t n, uint32_t *out) {
     constexpr int W = 64 / P;
@@ -71,8 +76,31 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
         for (int w = 0; w < WORK; ++w) acc = __builtin_amdgcn_perm(acc, acc + static_cast<uint32_t>(w), 0x05040302u + w);
     };
     const __amdgpu_buffer_rsrc_t rsout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(n * 4u), 0x00020000);
+    constexpr int NR = ST == 7 ? 4 : 16;
+    uint32_t rb[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) rb[i] = 0;
+    uint32_t nrb = 0, rb0 = 0;  // entries held; the block index of the oldest
+    auto flush = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int o = (int)(4u * ((lo & ~63u) + 64u * (rb0 + i)) + 4u * lane);
+            if (i >= NR - (int)nrb) __builtin_amdgcn_raw_buffer_store_b32(rb[i], rsout, o - 256 * (NR - (int)nrb), 0, 0);
+        }
+        rb0 += nrb;
+        nrb = 0;
+    };
     auto result = [&](uint32_t t) __attribute__((always_inline)) {  // after set t
         const int o = (int)(4u * ((lo + t * P) & ~63u) + 4u * lane);
+        if constexpr (ST >= 6) {
+            if ((t & 7u) == 7u) {
+#pragma unroll
+                for (int i = 0; i + 1 < NR; ++i) rb[i] = rb[i + 1];
+                rb[NR - 1] = acc;
+                nrb += nrb < NR ? 1u : 0u;
+                if (ST != 8 && ST != 9 && nrb == NR) flush();
+            }
+        }
         if constexpr (ST == 1 || ST == 4) {
             if ((t & 7u) == 7u) __builtin_amdgcn_raw_buffer_store_b32(acc, rsout, o, 0, ST == 4 ? 2 : 0);
         } else if constexpr (ST == 2 || ST == 5) {
@@ -84,7 +112,26 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
             }
         }
     };
-    if constexpr (DEPTH == 3) {
+    if constexpr (ST == 9) {  // passes of 128 sets (16 blocks), drained, then stored
+        for (uint32_t t0 = 0; t0 < nsets; t0 += 128) {
+            const uint32_t t1 = nsets - t0 < 128 ? nsets : t0 + 128;
+            load(t0, ua);
+            load(t0 + 1, ub);
+            for (uint32_t t = t0; t < t1; t += 3) {
+                load(t + 2 < t1 ? t + 2 : nsets, uc);
+                fold(ua);
+                result(t);
+                load(t + 3 < t1 ? t + 3 : nsets, ua);
+                fold(ub);
+                result(t + 1);
+                load(t + 4 < t1 ? t + 4 : nsets, ub);
+                fold(uc);
+                result(t + 2);
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the pass's loads are in
+            if (nrb) flush();
+        }
+    } else if constexpr (DEPTH == 3) {
         load(0, ua);
         load(1, ub);
         for (uint32_t t = 0; t < nsets; t += 3) {
@@ -109,6 +156,9 @@ __global__ __launch_bounds__(1024) void short_rows(const uint8_t *base, uint32_t
             result(t + 1);
         }
     }
+    if constexpr (ST >= 6 && ST != 9) {
+        if (nrb) flush();
+    }
     if (acc == 0x12345678u) out[0] = acc;
 }
 
@@ -128,15 +178,16 @@ float time_it(F f, int reps) {
     return ms / reps;
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const bool only_store = argc > 1 && argv[1][0] == 's';
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
     uint8_t *d;
     uint32_t *out;
-    const size_t cap = (size_t)1400 << 20;
+    const size_t cap = (size_t)5400 << 20;
     CK(hipMalloc(&d, cap));
-    CK(hipMalloc(&out, (size_t)4 << 22));
+    CK(hipMalloc(&out, (size_t)4 << 24));
     CK(hipMemset(d, 0x5a, cap));
     const int reps = 20;
     auto run = [&](const char *name, uint32_t L, uint32_t n, auto kern) {
@@ -147,6 +198,27 @@ int main() {
     };
     for (int round = 0; round < 2; ++round) {
         const uint32_t n316 = 4u << 20, n1084 = 1u << 20;
+        if (only_store) {  // the result-store shapes only
+            run("8 pkts/wave, 32-B dword rows, default", 316, n316, short_rows<8, 0, 10, 0>);
+            run("8 pkts/wave, 32-B dword rows, default, store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 1>);
+            run("8 pkts/wave, 32-B dword rows, default, store every set (OOR but 1 in 8)", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 2>);
+            run("8 pkts/wave, 32-B dword rows, default, 4 stores / 32 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 3>);
+            run("8 pkts/wave, 32-B dword rows, default, nt store / 8 sets", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 4>);
+            run("8 pkts/wave, 32-B dword rows, default, nt store every set (OOR but 1 in 8)", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 5>);
+            run("8 pkts/wave, 32-B dword rows, default, 16-register result buffer", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 6>);
+            run("8 pkts/wave, 32-B dword rows, default, 4-register result buffer", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 7>);
+            run("8 pkts/wave, 32-B dword rows, default, 16-register buffer stored after the loop", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 8>);
+            run("8 pkts/wave, 32-B dword rows, default, passes of 16 blocks, stored after each", 316, n316, short_rows<8, 0, 10, 0, 0, 3, 9>);
+            run("8 pkts/wave, 32-B dword rows, default, passes of 16 blocks, stored after each", 316, 4 * n316, short_rows<8, 0, 10, 0, 0, 3, 9>);
+            run("8 pkts/wave, 32-B dword rows, default, store / 8 sets", 316, 4 * n316, short_rows<8, 0, 10, 0, 0, 3, 1>);
+            run("8 pkts/wave, 32-B dword rows, default", 316, 4 * n316, short_rows<8, 0, 10, 0>);
+            run("8 pkts/wave, 32-B dword rows, default", 1084, n1084, short_rows<8, 0, 34, 0>);
+            run("8 pkts/wave, 32-B dword rows, default, store / 8 sets", 1084, n1084, short_rows<8, 0, 34, 0, 0, 3, 1>);
+            run("8 pkts/wave, 32-B dword rows, default, 16-register result buffer", 1084, n1084, short_rows<8, 0, 34, 0, 0, 3, 6>);
+            run("8 pkts/wave, 32-B dword rows, default, 16-register buffer stored after the loop", 1084, n1084, short_rows<8, 0, 34, 0, 0, 3, 8>);
+            run("8 pkts/wave, 32-B dword rows, default, passes of 16 blocks, stored after each", 1084, n1084, short_rows<8, 0, 34, 0, 0, 3, 9>);
+            continue;
+        }
         run("1 pkt/wave, 256-B dword rows, default", 316, n316, short_rows<1, 0, 2, 0>);
         run("1 pkt/wave, 256-B dword rows, nt", 316, n316, short_rows<1, 0, 2, 2>);
         run("2 pkts/wave, 128-B dword rows, default", 316, n316, short_rows<2, 0, 3, 0>);
