@@ -53,6 +53,11 @@ constexpr bool kOctPrio = true;
 constexpr bool kOctClampRows = true;            // a set's rows past its last one re-load that row
 constexpr int kOctPairs = 2;                    // ring positions of two frames: one pair in flight
 constexpr uint32_t kOctMaxL = 1088u;            // 34 rows, 4 frames: longer packets are the long kernel's
+// Block results are held in registers and stored kOctRes blocks at a time (and after the ring):
+// a store inside the ring sits in the same in-order vmcnt queue as the row loads, so every load
+// behind it waits for its write acknowledgement (scripts/shortbench.hip: one store per 8 sets
+// costs 19 % of the short-packet stream; this buffer: C2 -1.5-2.5 %, same-box A/B).
+constexpr int kOctRes = 8;
 
 // Frame descriptor (one per frame of a block, lane t of OctBlock::ftab; also the slot flags):
 constexpr uint32_t kFdSet = 7u;             // bits 0-2: the set (sorted positions 8 s .. 8 s + 7)
@@ -204,7 +209,7 @@ struct OctSlot {
     int kf;        // stream word of this lane in the set's row 0 (header masks), first frame
     int rl;        // rows of this lane's packet from this frame's row 0 (generic sets: the freeze)
     uint32_t rt;   // routing: lane i of the block takes the result of lane rt (0xFF: none), last frame
-    uint32_t rq;   // result store offset (the block's packet i, block's last frame), else OOR
+    uint32_t rq;   // the block (bits 0-30); bit 31: lane i of the block is not this kernel's packet
     uint32_t tro;  // trailer offset from the block base (lane 8g of a packet, last frame), else OOR
     uint64_t boff; // uniform (TRAILER only)
     uint32_t fl;   // uniform: the frame descriptor (kOct* flags, rrem in bits 24-31), 0 if empty
@@ -345,6 +350,32 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
 
     uint32_t acc_c = 0;  // accumulator carried from frame to frame
     uint32_t rbv = 0;    // the block result register (lane i = packet i of the block)
+    // finished blocks' results, not yet stored: entry e in rres[e] (the newest in rres[kOctRes -
+    // 1]), bit e of rown set where this lane's packet of entry e is this kernel's, lane e of rblk
+    // the entry's block; nres entries held
+    uint32_t rres[kOctRes];
+#pragma unroll
+    for (int e = 0; e < kOctRes; ++e) rres[e] = 0;
+    uint32_t rown = 0, rblk = 0;
+    int nres = 0;
+    // store entries [kOctRes - nres, kOctRes)
+    auto flush = [&]() __attribute__((always_inline)) {
+        if constexpr (DIAG == 5 || DIAG == 6) return;
+        const int e0 = kOctRes - nres;
+        const __amdgpu_buffer_rsrc_t os =
+            MODE == kCompute
+                ? __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0, 0x00020000)
+                : __builtin_amdgcn_make_buffer_rsrc(p.ok ? p.ok + lo : nullptr, 0, p.ok ? static_cast<int>(nq) : 0, 0x00020000);
+#pragma unroll
+        for (int e = 0; e < kOctRes; ++e) {
+            if (e >= e0) {
+                const uint32_t q = readlane_u32(rblk, e) * 64u + lane;
+                const uint32_t o = ((rown >> e) & 1u) ? q * (MODE == kCompute ? 4u : 1u) : kOctOOR;
+                if constexpr (MODE == kCompute) __builtin_amdgcn_raw_buffer_store_b32(rres[e], os, static_cast<int>(o), 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rres[e]), os, static_cast<int>(o), 0, 0);
+            }
+        }
+    };
 
     auto issue = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
@@ -420,8 +451,8 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         // takes group (pos_i & 7)'s result at the last frame of set pos_i >> 3
         const uint32_t pi = LB.pos;
         S.rt = (last && (pi >> 3) == set) ? (pi & 7u) << 3 : 0xFFu;
-        S.rq = ((fd & kOctBlockLast) && pi != 0xFFu) ? (static_cast<uint32_t>(LB.block) * 64u + lane) * (MODE == kCompute ? 4u : 1u)
-                                                    : kOctOOR;
+        // the block (uniform) in bits 0-30, bit 31: this lane's packet is not this kernel's
+        S.rq = static_cast<uint32_t>(LB.block) | (pi != 0xFFu ? 0u : kOctOOR);
         if constexpr (TRAILER) S.boff = boff;
         S.fl = fd;
         lt += have ? 1 : 0;
@@ -445,17 +476,19 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, ts, static_cast<int>(S.tro), 0, 0);
         }
-        // the block's results leave after its last set
+        // the block's results are complete after its last set: into the register buffer, which
+        // is stored when full (and after the ring)
         if (!(S.fl & kOctBlockLast)) return;
-        if constexpr (MODE == kCompute) {
-            const __amdgpu_buffer_rsrc_t os =
-                __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0,
-                                                  0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(rbv, os, static_cast<int>(S.rq), 0, 0);
-        } else {
-            const __amdgpu_buffer_rsrc_t os =
-                __builtin_amdgcn_make_buffer_rsrc(p.ok ? p.ok + lo : nullptr, 0, p.ok ? static_cast<int>(nq) : 0, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rbv), os, static_cast<int>(S.rq), 0, 0);
+#pragma unroll
+        for (int e = 0; e + 1 < kOctRes; ++e) rres[e] = rres[e + 1];
+        rres[kOctRes - 1] = rbv;
+        rown = (rown >> 1) | ((S.rq >> 31) ? 0u : 1u << (kOctRes - 1));
+        // lane e <- lane e + 1 (DPP wave_shl:1), the new entry's block in lane kOctRes - 1
+        rblk = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(rblk), 0x130, 0xF, 0xF, false));
+        rblk = lane == kOctRes - 1 ? (S.rq & 0x7FFFFFFFu) : rblk;
+        if (++nres == kOctRes) {
+            flush();
+            nres = 0;
         }
     };
 
@@ -540,6 +573,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             break;
         }
     }
+    if (nres) flush();
     if (bailed) {  // never reached by correct bookkeeping: make it loud, not silent
         for (uint32_t i = lane; i < nq; i += 64u) store_result<MODE>(p, lo + i, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN);
         if (p.nerr && lane == 0) atomicAdd(p.nerr, nq);
