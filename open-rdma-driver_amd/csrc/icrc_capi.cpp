@@ -689,22 +689,27 @@ int icrc_engine_create(int device, icrc_engine **out) {
         return ICRC_EDEVICE;
     }
     e->num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
-    std::vector<uint32_t> img(icrc::kLdsWords), img_oct(icrc::kLdsWords);
+    // each device table buffer: the full LDS image, then its compact form (icrc_internal.h)
+    constexpr size_t kBufBytes = icrc::kTableBufWords * 4u;
+    std::vector<uint32_t> img(icrc::kTableBufWords), img_oct(icrc::kTableBufWords);
     icrc::build_table_image(img.data());
+    icrc::append_compact_image(img.data());
     icrc::build_table_image_oct(img_oct.data());
+    icrc::append_compact_image(img_oct.data());
 #ifdef ICRC_AB_BUILD  // the quad kernels' image (A/B library only)
-    std::vector<uint32_t> img_quad(icrc::kLdsWords);
+    std::vector<uint32_t> img_quad(icrc::kTableBufWords);
     icrc::build_table_image_quad(img_quad.data());
-    if (hipMalloc(&e->d_table_quad, icrc::kLdsBytes) != hipSuccess ||
-        hipMemcpy(e->d_table_quad, img_quad.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess) {
+    icrc::append_compact_image(img_quad.data());
+    if (hipMalloc(&e->d_table_quad, kBufBytes) != hipSuccess ||
+        hipMemcpy(e->d_table_quad, img_quad.data(), kBufBytes, hipMemcpyHostToDevice) != hipSuccess) {
         icrc_engine_destroy(e);
         return ICRC_EDEVICE;
     }
 #endif
-    if (hipMalloc(&e->d_table, icrc::kLdsBytes) != hipSuccess ||
-        hipMemcpy(e->d_table, img.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc(&e->d_table_oct, icrc::kLdsBytes) != hipSuccess ||
-        hipMemcpy(e->d_table_oct, img_oct.data(), icrc::kLdsBytes, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMalloc(&e->d_table, kBufBytes) != hipSuccess ||
+        hipMemcpy(e->d_table, img.data(), kBufBytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&e->d_table_oct, kBufBytes) != hipSuccess ||
+        hipMemcpy(e->d_table_oct, img_oct.data(), kBufBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||

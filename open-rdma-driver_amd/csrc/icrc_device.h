@@ -279,6 +279,44 @@ __device__ __forceinline__ uint32_t wave_chunk(uint32_t n, uint32_t tw) {
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
 }
+// ---- the table image into LDS ------------------------------------------------------------
+// From its compact form (icrc_internal.h, stored after the full image): thread t of the
+// 1024-thread workgroup reads bulk entry t = B_b[x] (b = t >> 8, x = t & 255) and writes its 32
+// bank copies (128 contiguous bytes) as eight 16-byte stores, the k-th at chunk (k + x) & 7 so
+// that neighbouring lanes write different banks; plus two 16-byte pieces of the final tables.
+// table_fetch only issues the loads (a kernel can issue its first packet loads before it waits
+// for them); table_store writes LDS and joins the workgroup barrier.
+struct TableShare {
+    uint32_t bulk;
+    uint4 fin[2];
+};
+static_assert(kThreadsPerGroup == 1024 && (kLdsBytes - kFinalBase) == 2u * 16u * kThreadsPerGroup, "table share");
+__device__ __forceinline__ void table_fetch(TableShare &t, const uint32_t *table) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(table + kLdsWords), 0,
+                                                                        static_cast<int>(kCompactWords * 4u), 0x00020000);
+    t.bulk = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(4u * threadIdx.x), 0, 0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(4096u + 16u * (threadIdx.x + k * 1024u)), 0, 0);
+        t.fin[k] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+__device__ __forceinline__ void table_store(const TableShare &t, uint4 *lds4) {
+    const uint32_t b = threadIdx.x >> 8, x = threadIdx.x & 255u;
+    const uint32_t row = ((b >> 1) * 65536u + x * 256u + (b & 1u) * 128u) / 16u;  // first uint4 of the 32 copies
+    const uint4 v = make_uint4(t.bulk, t.bulk, t.bulk, t.bulk);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) lds4[row + ((k + x) & 7u)] = v;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) lds4[kFinalBase / 16u + threadIdx.x + k * 1024u] = t.fin[k];
+    __syncthreads();
+}
+__device__ __forceinline__ void table_fill(uint4 *lds4, const uint32_t *table) {
+    TableShare t;
+    table_fetch(t, table);
+    table_store(t, lds4);
+}
+
 constexpr int kStreamAux = 2;  // nt: packets are read once (MI355X_MICROARCH.md nt-weights); +7 % on C1
 
 // ---- helpers of the multi-packet-per-wave kernels (icrc_quad.hip, icrc_oct.hip) ----------------

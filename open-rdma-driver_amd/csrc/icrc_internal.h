@@ -26,6 +26,14 @@ void build_table_image(uint32_t *img);
 void build_table_image_quad(uint32_t *img);
 // Oct image (eight packets per wavefront, 8 lanes each): M^8 bulk, M^(8 - (l & 7)) final.
 void build_table_image_oct(uint32_t *img);
+// Compact image, stored in HBM right after each full image (the device buffer holds
+// kLdsWords + kCompactWords words): the 1024 distinct bulk entries (word b * 256 + x = B_b[x]),
+// then the 32 KiB final tables exactly as at kFinalBase.  A workgroup reads these 36 KiB and
+// replicates the bulk entries 32x into LDS itself (table_fill, icrc_device.h) instead of reading
+// the 160 KiB image: 256 workgroups x 160 KiB = 40 MiB of table reads per launch becomes 9 MiB.
+constexpr uint32_t kCompactWords = 1024u + (kLdsBytes - kFinalBase) / 4u;
+constexpr uint32_t kTableBufWords = kLdsWords + kCompactWords;
+void append_compact_image(uint32_t *img);  // img[kLdsWords ..] <- compact form of img[0 .. kLdsWords)
 // Host reference helpers used by the table builder (exposed for unit tests).
 uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
 

@@ -48,13 +48,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
 template <int MODE, int S, int D, int ABL, bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
-    }
-    __syncthreads();
     const char *lds = reinterpret_cast<const char *>(lds4);
-
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     LaneConsts c;
@@ -64,6 +58,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
     const uint32_t tw = gridDim.x * kWavesPerGroup;
     const uint32_t gw = p.spread ? wave * gridDim.x + blockIdx.x : blockIdx.x * kWavesPerGroup + wave;
     if constexpr (S == 0) {
+        table_fill(lds4, p.table);
         for (uint32_t i = gw; i < p.n; i += tw) {
             const uint64_t off = p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride;
             const uint32_t L = p.len ? p.len[i] : p.ulen;
@@ -71,13 +66,14 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
             if (lane == 0) store_result<MODE>(p, i, r);
         }
     } else {
-        // contiguous chunks, 64-packet aligned so result stores are whole blocks
+        // contiguous chunks, 64-packet aligned so result stores are whole blocks; the table
+        // image is loaded inside run_pipelined<TABLE>, overlapped with the first row loads
+        TableShare tv;
         const uint32_t chunk = wave_chunk(p.n, tw);
         const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
-        if (lo64 >= p.n) return;
-        const uint32_t lo = static_cast<uint32_t>(lo64);
+        const uint32_t lo = lo64 < p.n ? static_cast<uint32_t>(lo64) : p.n;
         const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-        run_pipelined<MODE, S, D, ABL, 0, false, TRAILER>(p, lds, c, lane, lo, nq);
+        run_pipelined<MODE, S, D, ABL, 0, false, TRAILER, true>(p, lds, c, lane, lo, nq, &tv);
     }
 }
 
@@ -88,11 +84,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
 template <int S, int D, bool TRAILER, int PARSE>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
-    }
-    __syncthreads();
+    table_fill(lds4, p.table);
     const char *lds = reinterpret_cast<const char *>(lds4);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -437,11 +429,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                                                                           uint32_t *pkt_len,
                                                                           uint32_t *icrc_out, const uint32_t *table) {
     __shared__ uint4 lds4[kLdsBytes / 16];
-    {
-        const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = t4[i];
-    }
-    __syncthreads();
+    table_fill(lds4, table);
     const char *lds = reinterpret_cast<const char *>(lds4);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

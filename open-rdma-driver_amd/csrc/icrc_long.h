@@ -530,12 +530,17 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // (S independent CRC chains for ILP); the loads of set t + D are issued before set t is
 // processed (a D-deep register ring), keeping ~D*S packets in flight per wave against the
 // ~3 us loaded HBM latency.  Results leave 64 at a time as coalesced stores.
-template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false, bool TRAILER = false>
+// TABLE: the table image is not in LDS yet.  The wave issues its first (offset, length) block
+// (ragged batches), its share of the table image (into `tv`) and its first sets' row loads before
+// it waits for the table share, so that the three memory latencies overlap (a small batch, one
+// packet per wave, is made of little else); then every wave, with or without packets, writes its
+// share to LDS and joins the barrier.
+template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false, bool TRAILER = false, bool TABLE = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
-                                              uint32_t lane, uint32_t lo, uint32_t nq) {
+                                              uint32_t lane, uint32_t lo, uint32_t nq, TableShare *tv = nullptr) {
     constexpr int B = D + 1;
     static_assert(64 % S == 0, "sets must not straddle a 64-packet result block");
-    if (nq == 0) return;
+    if (!TABLE && nq == 0) return;
     const uint32_t nsets = (nq + S - 1) / S;
     const bool ragged = p.off != nullptr || p.len != nullptr;
     MetaBlock mb;
@@ -550,15 +555,25 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
+    if constexpr (TABLE) {
+        if (ragged && nq != 0) meta_fetch(p, mb, lo, lo + nq, 0, lane);
+        table_fetch(*tv, p.table);
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        if (static_cast<uint32_t>(d) < nsets) {
+        // TABLE: unconditional (an empty slot's loads are out of range), so that the wait for the
+        // table share below counts exactly these loads behind it
+        if (TABLE || static_cast<uint32_t>(d) < nsets) {
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 slot_meta<LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
                 slot_load<ABL, MODE, TRAILER>(m[d][s], lane, u[d][s]);
             }
         }
+    }
+    if constexpr (TABLE) {
+        table_store(*tv, const_cast<uint4 *>(reinterpret_cast<const uint4 *>(lds)));
+        if (nq == 0) return;
     }
     for (uint32_t t = 0; t < nsets; t += B) {
         const bool cont = static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
@@ -733,11 +748,7 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint64_t g0 = static_cast<uint64_t>(bid) * per, g1 = g0 + per < p.n ? g0 + per : p.n;
         if (!wg_any_split<false>(p, lds4, g0, g1)) return;
     }
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.table);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
-    }
-    __syncthreads();
+    table_fill(lds4, p.table);
     const char *lds = reinterpret_cast<const char *>(lds4);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

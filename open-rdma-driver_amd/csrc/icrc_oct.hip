@@ -614,11 +614,7 @@ __device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint
         const uint64_t end = g1 < p.n ? g1 : p.n;
         if (!wg_any_split<true>(p, lds4, g0, end)) return;
     }
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.table_oct);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kThreadsPerGroup) lds4[i] = src[i];
-    }
-    __syncthreads();
+    table_fill(lds4, p.table_oct);
     const char *lds = reinterpret_cast<const char *>(lds4);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

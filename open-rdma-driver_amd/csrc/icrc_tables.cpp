@@ -75,6 +75,13 @@ static void build_image(uint32_t *img, uint32_t W) {
     }
 }
 
+void append_compact_image(uint32_t *img) {
+    uint32_t *c = img + kLdsWords;
+    for (uint32_t b = 0; b < 4; b++)
+        for (uint32_t x = 0; x < 256; x++) c[b * 256u + x] = img[((b >> 1) * 65536u + x * 256u + (b & 1u) * 128u) / 4u];
+    std::memcpy(c + 1024, img + kFinalBase / 4u, kLdsBytes - kFinalBase);
+}
+
 void build_table_image(uint32_t *img) { build_image(img, 64); }
 
 void build_table_image_quad(uint32_t *img) { build_image(img, 16); }

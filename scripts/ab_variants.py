@@ -43,6 +43,25 @@ def main():
             jobs["C1"] = (lambda b1=b1, out1=out1, n=w1.n, L=L: eng.compute_strided(b1.data_ptr(), L, L, n, out1.data_ptr(),
                                                                                    False, s), w1.n * L, out1)
             continue
+        if name in ("C3", "C3c") or name.startswith("W"):
+            # 16 MiB WRITE: compute (write trailers) + verify (zero trailers) / compute only;
+            # Wk: a WRITE of k 4 KiB packets, compute only (as C3c)
+            w3 = workloads.write_message((int(name[1:]) if name.startswith("W") else 4096) * 4096, 4096)
+            b3 = workloads.synthesize(eng, w3, stream=s)
+            o3, l3 = dev(w3.off), dev(w3.lens)
+            out3 = torch.zeros(w3.n, dtype=torch.int32, device="cuda")
+            ok3 = torch.zeros(w3.n, dtype=torch.uint8, device="cuda")
+            keep += [b3, o3, l3, out3, ok3]
+
+            def rt(b3=b3, o3=o3, l3=l3, out3=out3, ok3=ok3, n=w3.n, both=name == "C3"):
+                eng.compute_batch(b3.data_ptr(), o3.data_ptr(), l3.data_ptr(), n, out3.data_ptr(), both, 0, s)
+                if both:
+                    eng.verify_batch(b3.data_ptr(), o3.data_ptr(), l3.data_ptr(), n, ok3.data_ptr(), True, 0, s)
+            nb3 = int(w3.lens.astype(np.uint64).sum()) * (2 if name == "C3" else 1)
+            if name.startswith("W"):
+                name = f"W{w3.n}"
+            jobs[name] = (rt, nb3, out3)
+            continue
         kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0),
               "C2m": dict(classes=(256, 1024)), "C2snr": dict(classes=(256,), ragged_frac=0.0)}[name]
         w2 = workloads.mixed_mtu_stream(4 << 20, **kw)
