@@ -348,7 +348,7 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
     return fails, checked
 
 
-PMC_TRAFFIC_FILE = "r02_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r03_pmc_traffic.json"
 LOADS_ONLY_VARIANT = 19  # A/B library: icrc_batch_kernel<.., S = 2, D = 1, loads only>, the default ring without the CRC
 
 
