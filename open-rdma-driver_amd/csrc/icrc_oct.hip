@@ -305,9 +305,16 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
 // without the per-frame stores, 7 = the full kernel without the final products, 8 = the full
 // kernel with each set's per-lane packet data taken from the lane itself (no bperm before the
 // loads).
-template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
+// 9 / 10 = the full kernel / the loads-only build with each set's per-lane packet data computed
+// from the index (strided uniform batches only: no ds_bpermute on the path to a frame's loads;
+// wrong on anything else); 11 = the full kernel without the raised wave priority.
+constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11) ? 0 : d; }
+template <int MODE, bool RAGGED, bool TRAILER, int DIAGX>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
+    constexpr int DIAG = oct_diag_base(DIAGX);
+    constexpr bool kArithSetup = DIAGX == 9 || DIAGX == 10;
+    constexpr bool kPrio = kOctPrio && DIAGX != 11;
     constexpr int K = kOctK;
     constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
     constexpr int B = 2 * P;
@@ -380,7 +387,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     auto issue = [&](auto bc) __attribute__((always_inline)) {
         constexpr int b = decltype(bc)::value;
         OctSlot<MODE, TRAILER> &S = sl[b];
-        if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(3);  // the frame's setup gates its loads
+        if constexpr (kPrio) __builtin_amdgcn_s_setprio(3);  // the frame's setup gates its loads
         if (lt >= lnfr) {  // the block is issued: the next one, if prepared
             if (nb_ready) {
                 LB = NB;
@@ -398,9 +405,16 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             const uint32_t ps = 8u * set + grp;
             // DIAG 8: this lane's own block entry instead of the set's (no LDS round trip on the
             // path to the loads; wrong results by design)
-            const uint32_t key = DIAG == 8 ? LB.key : bperm(ps, LB.key);
-            const uint32_t vrel = DIAG == 8 ? LB.vrel : bperm(ps, LB.vrel);
-            const uint32_t L = DIAG == 8 ? LB.len : bperm(ps, LB.len);
+            uint32_t key, vrel, L;
+            if constexpr (kArithSetup) {
+                L = p.ulen;
+                key = (((1u + ((L - 4u) >> 2) + 7u) >> 3) << 6) | ps;
+                vrel = ps * static_cast<uint32_t>(p.stride);
+            } else {
+                key = DIAG == 8 ? LB.key : bperm(ps, LB.key);
+                vrel = DIAG == 8 ? LB.vrel : bperm(ps, LB.vrel);
+                L = DIAG == 8 ? LB.len : bperm(ps, LB.len);
+            }
             lreal = ps < static_cast<uint32_t>(__popcll(LB.mine));
             const uint32_t N = 1u + ((L - 4u) >> 2);
             const int z = static_cast<int>((8u - (N & 7u)) & 7u);
@@ -439,7 +453,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 const uint32_t so = kOctClampRows ? (32u * (j - 1) < cap ? 32u * (j - 1) : cap) : 32u * (j - 1);
                 S.u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(o1), static_cast<int>(so), 0);
             }
-            if constexpr (kOctPrio) __builtin_amdgcn_s_setprio(0);
+            if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         }
         const bool last = (fd & kOctLast) != 0u;
         if constexpr (MODE == kVerify)
@@ -666,6 +680,9 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
         case 5: ICRC_O(M, R, false, 5); break;                       \
         case 6: ICRC_O(M, R, false, 6); break;                       \
         case 7: ICRC_O(M, R, false, 7); break;                       \
+        case 9: ICRC_O(M, R, false, 9); break;                       \
+        case 10: ICRC_O(M, R, false, 10); break;                     \
+        case 11: ICRC_O(M, R, false, 11); break;                     \
         default: ICRC_O(M, R, false, 8); break;                      \
         }                                                            \
     } while (0)

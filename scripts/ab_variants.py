@@ -2,7 +2,7 @@
 """A/B the ICRC kernel variants in ONE process, interleaved rounds (methodology rule 24):
 C1 (1 Mi x 4156 B, strided) and C2 (mixed MTU, ragged) for each variant; checks that every
 variant returns identical ICRCs.  Prints one JSON line per (workload, variant)."""
-DIAGNOSTIC = {15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48}  # ablations (loads-only / CRC-only / no loads): wrong results by design
+DIAGNOSTIC = {15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 50}  # ablations (loads-only / CRC-only / no loads): wrong results by design
 import json
 import os
 import sys
@@ -34,13 +34,13 @@ def main():
     jobs = {}
     keep = []
     for name in os.environ.get("JOBS", "C1,C2").split(","):
-        if name == "C1":
-            w1 = workloads.write_middle_stream(1 << 20)
+        if name in ("C1", "S316"):  # S316: 4 Mi strided 316-byte packets (the 256-B MTU class)
+            w1 = workloads.write_middle_stream(1 << 22, pmtu=256) if name == "S316" else workloads.write_middle_stream(1 << 20)
             L = int(w1.lens[0])
             b1 = workloads.synthesize(eng, w1, stream=s)
             out1 = torch.zeros(w1.n, dtype=torch.int32, device="cuda")
             keep += [b1, out1]
-            jobs["C1"] = (lambda b1=b1, out1=out1, n=w1.n, L=L: eng.compute_strided(b1.data_ptr(), L, L, n, out1.data_ptr(),
+            jobs[name] = (lambda b1=b1, out1=out1, n=w1.n, L=L: eng.compute_strided(b1.data_ptr(), L, L, n, out1.data_ptr(),
                                                                                    False, s), w1.n * L, out1)
             continue
         if name in ("C3", "C3c") or name.startswith("W"):
