@@ -152,7 +152,17 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     p.split_len = split;
     // Default: both halves in one launch (the fused hybrid kernel).  A forced hybrid variant
     // (100 + q, 200 + q: A/B) keeps the two-stream fork / join below.
-    if (!hybrid_forced) return icrc::launch_hybrid(mode, p, grid, grid, stream);
+    if (!hybrid_forced) {
+        int grid_long = grid;
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_LONG_GRID = long-packet workgroups per oct workgroup
+        static const int long_mult = [] {
+            const char *v = std::getenv("ICRC_AB_LONG_GRID");
+            return v ? std::max(1, std::atoi(v)) : 1;
+        }();
+        grid_long = grid * long_mult;
+#endif
+        return icrc::launch_hybrid(mode, p, grid, grid_long, stream);
+    }
     std::lock_guard<std::mutex> g(e->fork_mu);
     HIP_TRY(hipEventRecord(e->fork_ev, static_cast<hipStream_t>(stream)));
     HIP_TRY(hipStreamWaitEvent(e->side, e->fork_ev, 0));
