@@ -279,6 +279,19 @@ __device__ __forceinline__ uint32_t wave_chunk(uint32_t n, uint32_t tw) {
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
 }
+// ---- verify as a compute over the trailer -------------------------------------------------
+// The ICRC is CRC-32/ISO-HDLC and the trailer holds it little-endian, so the ICRC computed over
+// the packet WITH its trailer as the stream's last word is the CRC-32 residue 0x2144DF1C exactly
+// when the trailer is right (is_icrc_valid, packet_processor.rs:341-353).  The pipelined kernels
+// verify that way: the trailer is one more stream word of the rows they load anyway, instead of a
+// load of its own.  Stream words: compute 1 + (L - 4) / 4 (the FF prefix word and the bytes
+// before the trailer), verify one more.
+constexpr uint32_t kIcrcResidue = 0x2144DF1Cu;
+template <int MODE>
+__device__ __forceinline__ uint32_t stream_words(uint32_t L) {
+    return MODE == kVerify ? 1u + (L >> 2) : 1u + ((L - 4u) >> 2);
+}
+
 // ---- the table image into LDS ------------------------------------------------------------
 // From its compact form (icrc_internal.h, stored after the full image): thread t of the
 // 1024-thread workgroup reads bulk entry t = B_b[x] (b = t >> 8, x = t & 255) and writes its 32

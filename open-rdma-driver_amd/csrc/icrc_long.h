@@ -53,7 +53,7 @@ __device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, 
 
 // LONG: the long-packet half of a split batch — packets with L < p.split_len belong to the short-
 // packet kernel and leave the slot empty (kind 0: no loads, no result).
-template <bool LONG = false>
+template <int MODE, bool LONG = false>
 __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, bool ragged, uint32_t lo,
                                           uint32_t q, uint32_t nq, uint32_t lane, SlotMeta &m) {
     m.kind = 0;
@@ -79,7 +79,7 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
     m.L = L;
     m.kind = 2;
     if (L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(m.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
-        const int N = 1 + static_cast<int>((L - 4u) >> 2);
+        const int N = static_cast<int>(stream_words<MODE>(L));
         const int R = (N + 63) >> 6;
         if (R <= kRows) {
             m.kind = 1;
@@ -103,11 +103,10 @@ constexpr int abl_mode(int abl) { return abl & 3; }
 constexpr int abl_aux(int abl) { return (abl >> 2) & 0x3F; }
 constexpr bool abl_prio(int abl) { return (abl & kAblNoPrio) == 0; }
 
-// Verify also loads the packet's stored trailer (all lanes, one dword) as load kRows of the same
-// ring position, so that the comparison needs no load of its own after the CRC (a load issued
-// there is the youngest in flight and its wait drains the ring).
+// Verify runs over the trailer as the stream's last word (kIcrcResidue, icrc_device.h): the same
+// kRows loads per slot as compute.
 template <int MODE>
-constexpr int ring_words() { return MODE == kVerify ? kRows + 1 : kRows; }
+constexpr int ring_words() { return kRows; }
 
 // TRAILER: the row holding the trailer's line (the last) and the verify trailer word load with the
 // default policy, so the line is in L2 when the trailer store / zeroing follows
@@ -132,12 +131,10 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
     for (int j = 0; j < kRows - 1; ++j)
         u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * j), 0, kAux);
     u[kRows - 1] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(vbase + 256u * (kRows - 1)), 0, kAuxLast);
-    if constexpr (MODE == kVerify)
-        u[kRows] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(m.L - 4u), 0, kAuxLast);
 }
 
 // Result of a regular packet of the pipelined path, from registers only: compute -> the ICRC;
-// verify -> OK / MISMATCH against the trailer word loaded with the rows.  TRAILER: the one
+// verify -> OK / MISMATCH: the ICRC over the packet with its trailer against kIcrcResidue.  TRAILER: the one
 // trailer store of the packet (compute: the ICRC, PacketWriter::write, packet_processor.rs:263;
 // verify: zeros, is_icrc_valid, 350) as a buffer store that every lane issues, lane 0 in range
 // (no branch, so the ring's vmcnt accounting stays exact; an empty slot's descriptor has size 0).
@@ -149,8 +146,9 @@ __device__ __forceinline__ uint32_t regular_result(const SlotMeta &m, uint32_t c
         __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs,
                                               static_cast<int>(lane == 0 ? m.L - 4u : 0x80000000u), 0, 0);
     }
+    (void)stored;
     if constexpr (MODE == kCompute) return crc;
-    else return stored == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+    else return crc == kIcrcResidue ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -503,8 +501,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         for (int s = 0; s < S; ++s) fin[s] = (ABL & kAblNoFinal) ? acc[s] : final_mul(lds, acc[s], c.fin);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]),
-                                                             MODE == kVerify ? u[s][ring_words<MODE>() - 1] : 0u, lane);
+            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]), 0u, lane);
             if (m[s].kind == 1) {
                 rb_put(rb, q0 + s, r);
                 if constexpr (PARSE == 1)
@@ -566,7 +563,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
         if (TABLE || static_cast<uint32_t>(d) < nsets) {
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta<LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
+                slot_meta<MODE, LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
                 slot_load<ABL, MODE, TRAILER>(m[d][s], lane, u[d][s]);
             }
         }
@@ -588,7 +585,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta<LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                slot_meta<MODE, LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
                 slot_load<ABL, MODE, TRAILER>(m[bp][s], lane, u[bp][s]);
             }
             if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(0);
@@ -667,7 +664,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
             sm.L = L;
             sm.kind = 2;
             if (((reinterpret_cast<uintptr_t>(sm.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
-                const int N = 1 + static_cast<int>((L - 4u) >> 2);
+                const int N = static_cast<int>(stream_words<MODE>(L));
                 const int R = (N + 63) >> 6;
                 if (R <= kRows) {
                     sm.kind = 1;

@@ -110,6 +110,7 @@ constexpr uint64_t kOctBaseSlack = 1ull << 30;  // block base: 1 GiB below its f
 // Classify block b from this lane's (offset, L): which packets are this kernel's, their row
 // counts, the block's base offset and extent; sort by row count.  Returns the ballot of packets
 // that are neither this kernel's nor the long-packet kernel's (the tail loop's).
+template <int MODE>
 __device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B, uint64_t off, uint32_t L, bool valid,
                                               uint32_t lo, int b, uint32_t lane) {
     const bool foreign = valid && p.split_len != 0 && L >= p.split_len;  // the long-packet kernel's
@@ -127,7 +128,7 @@ __device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B,
     }
     mine = mine && off >= boff && (off - boff) + L <= kOctRelLimit;
     const uint32_t vrel = static_cast<uint32_t>(off - boff);
-    const uint32_t R = mine ? (1u + ((L - 4u) >> 2) + 7u) >> 3 : kOctNotMine;
+    const uint32_t R = mine ? (stream_words<MODE>(L) + 7u) >> 3 : kOctNotMine;
     // sort (R << 6 | index) ascending: LSD radix over the bits of R that vary, one ballot and one
     // ds_permute per bit (skipped when the block is already in order)
     uint32_t key = (R << 6) | lane;
@@ -187,6 +188,7 @@ __device__ __forceinline__ uint64_t oct_block(const BatchParams &p, OctBlock &B,
 }
 
 // The tail loop's classification (reads (offset, L) from the batch arrays).
+template <int MODE>
 __device__ __forceinline__ uint64_t oct_classify(const BatchParams &p, uint32_t lo, uint32_t nq, int b, uint32_t lane,
                                                  uint64_t &off, uint32_t &L) {
     const uint32_t q = static_cast<uint32_t>(b) * 64u + lane;
@@ -199,13 +201,13 @@ __device__ __forceinline__ uint64_t oct_classify(const BatchParams &p, uint32_t 
         L = p.len ? p.len[i] : p.ulen;
     }
     OctBlock B;
-    return oct_block(p, B, off, L, valid, lo, b, lane);
+    return oct_block<MODE>(p, B, off, L, valid, lo, b, lane);
 }
 
 // One ring slot = one frame of one set (per-lane values in VGPRs, the frame descriptor in an SGPR).
 template <int MODE, bool TRAILER>
 struct OctSlot {
-    uint32_t u[MODE == kVerify ? kOctK + 1 : kOctK];  // frame rows (+ the stored trailer, lane 8g)
+    uint32_t u[kOctK];  // frame rows (verify: the trailer is the stream's last word, kIcrcResidue)
     int kf;        // stream word of this lane in the set's row 0 (header masks), first frame
     int rl;        // rows of this lane's packet from this frame's row 0 (generic sets: the freeze)
     uint32_t rt;   // routing: lane i of the block takes the result of lane rt (0xFF: none), last frame
@@ -408,7 +410,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             uint32_t key, vrel, L;
             if constexpr (kArithSetup) {
                 L = p.ulen;
-                key = (((1u + ((L - 4u) >> 2) + 7u) >> 3) << 6) | ps;
+                key = (((stream_words<MODE>(L) + 7u) >> 3) << 6) | ps;
                 vrel = ps * static_cast<uint32_t>(p.stride);
             } else {
                 key = DIAG == 8 ? LB.key : bperm(ps, LB.key);
@@ -416,7 +418,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 L = DIAG == 8 ? LB.len : bperm(ps, LB.len);
             }
             lreal = ps < static_cast<uint32_t>(__popcll(LB.mine));
-            const uint32_t N = 1u + ((L - 4u) >> 2);
+            const uint32_t N = stream_words<MODE>(L);
             const int z = static_cast<int>((8u - (N & 7u)) & 7u);
             lr = static_cast<int>(key >> 6);
             lkf = col - z;
@@ -456,8 +458,6 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         }
         const bool last = (fd & kOctLast) != 0u;
-        if constexpr (MODE == kVerify)
-            S.u[K] = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(last ? ltr : kOctOOR), 0, 0);
         S.kf = lkf;
         S.rl = lr - K * static_cast<int>(lf);
         S.tro = last ? ltr : kOctOOR;
@@ -477,7 +477,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     auto finish = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
         uint32_t r;
         if constexpr (MODE == kCompute) r = crc;
-        else r = bperm(grp << 3, S.u[K]) == crc ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
+        else r = crc == kIcrcResidue ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;  // over the trailer too
         const uint32_t v = bperm(S.rt & 63u, r);
         rbv = S.rt != 0xFFu ? v : rbv;
     };
@@ -555,7 +555,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                             : static_cast<uint64_t>(lo + q) * p.stride;
                 L = p.len ? m_len : p.ulen;
             }
-            if (oct_block(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
+            if (oct_block<MODE>(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
             nb_next += 1;
             nb_ready = NB.nfr > 0;
         }
@@ -598,7 +598,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         for (int b = 0; b < nblocks; ++b) {
             uint64_t off;
             uint32_t L;
-            uint64_t m = oct_classify(p, lo, nq, b, lane, off, L);
+            uint64_t m = oct_classify<MODE>(p, lo, nq, b, lane, off, L);
             while (m) {
                 const int l = __builtin_ctzll(m);
                 m &= m - 1;

@@ -34,6 +34,17 @@ def main():
     jobs = {}
     keep = []
     for name in os.environ.get("JOBS", "C1,C2").split(","):
+        if name in ("C1v", "S316v"):  # verify (is_icrc_valid) of the strided batches, trailers written first
+            w1 = workloads.write_middle_stream(1 << 22, pmtu=256) if name == "S316v" else workloads.write_middle_stream(1 << 20)
+            L = int(w1.lens[0])
+            b1 = workloads.synthesize(eng, w1, stream=s)
+            scratch = torch.zeros(w1.n, dtype=torch.int32, device="cuda")
+            eng.compute_strided(b1.data_ptr(), L, L, w1.n, scratch.data_ptr(), True, s)  # write the trailers
+            ok1 = torch.zeros(w1.n, dtype=torch.uint8, device="cuda")
+            keep += [b1, scratch, ok1]
+            jobs[name] = (lambda b1=b1, ok1=ok1, n=w1.n, L=L: eng.verify_strided(b1.data_ptr(), L, L, n, ok1.data_ptr(),
+                                                                               False, s), w1.n * L, ok1)
+            continue
         if name in ("C1", "S316"):  # S316: 4 Mi strided 316-byte packets (the 256-B MTU class)
             w1 = workloads.write_middle_stream(1 << 22, pmtu=256) if name == "S316" else workloads.write_middle_stream(1 << 20)
             L = int(w1.lens[0])
