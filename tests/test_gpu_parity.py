@@ -1276,3 +1276,72 @@ def test_hybrid_segregated_halves(engine, variant):
         assert all(not zb[int(o) + int(L) - 4: int(o) + int(L)].any() for o, L in zip(off, lens))
     finally:
         engine.set_variant(-1)
+
+
+def _residue_boundary_lengths():
+    """Packet lengths (4-byte multiples) where the verify stream (1 + L / 4 words: the trailer is
+    its last word, kIcrcResidue) crosses a row boundary of the oct kernel (8-word rows, 10-row
+    frames, L <= 1088) or of the one-packet pipeline (64-word rows, 17 rows: L <= 4348 on the fast
+    path, 4352 and up on the byte-wise one)."""
+    ls = set(range(44, 1201, 4))
+    for k in range(1, 19):
+        for nv in (64 * k - 1, 64 * k, 64 * k + 1):
+            L = 4 * (nv - 1)
+            if L >= 44:
+                ls.add(L)
+    ls.update(range(4336, 4372, 4))
+    return np.array(sorted(ls), np.uint32)
+
+
+@pytest.mark.parametrize("variant", [-1, 16, 40])
+@pytest.mark.parametrize("zero_trailer", [False, True])
+def test_verify_residue_row_boundaries(engine, variant, zero_trailer):
+    """Verify runs as a compute over the packet and its trailer (ICRC residue 0x2144DF1C): every
+    row-boundary length of both kernels, right trailers, a flipped payload bit, a flipped trailer
+    bit, ragged (default hybrid dispatch or a forced kernel) and strided per length."""
+    rng = np.random.default_rng(7 + variant + (1000 if zero_trailer else 0))
+    lens = np.repeat(_residue_boundary_lengths(), 2)
+    n = lens.size
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    tr = (off + lens.astype(np.uint64) - 4).astype(np.int64)[:, None] + np.arange(4)
+    buf[tr] = oracle_icrcs(buf, off, lens).view(np.uint8).reshape(-1, 4)
+    bad_payload = rng.choice(n, 40, replace=False)
+    bad_trailer = np.setdiff1d(rng.choice(n, 40, replace=False), bad_payload)
+    for i in bad_payload:
+        buf[int(off[i]) + 40 + int(rng.integers(0, int(lens[i]) - 44))] ^= 0x10
+    for i in bad_trailer:
+        buf[int(off[i] + lens[i]) - 4 + int(rng.integers(0, 4))] ^= 0x01
+    want = np.ones(n, np.uint8)
+    want[bad_payload] = 0
+    want[bad_trailer] = 0
+    engine.set_variant(variant)
+    try:
+        d_b, d_o, d_l = dev(buf), dev(off), dev(lens)
+        d_ok = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        engine.verify_batch(d_b.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), n, d_ok.data_ptr(), zero_trailer=zero_trailer,
+                            stream=stream_handle())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_ok.cpu().numpy(), want)
+        if zero_trailer:
+            assert not d_b.cpu().numpy()[tr].any()
+        # strided, one batch per length (the strided dispatch: oct below 1089 B, one packet per wave above)
+        for L in (44, 316, 1084, 1088, 1092, 4152, 4156, 4348, 4352):
+            m = 96
+            sb = rng.integers(0, 256, m * L, dtype=np.uint8)
+            so = np.arange(m, dtype=np.uint64) * L
+            sl = np.full(m, L, np.uint32)
+            str_ = (so + L - 4).astype(np.int64)[:, None] + np.arange(4)
+            sb[str_] = oracle_icrcs(sb, so, sl).view(np.uint8).reshape(-1, 4)
+            sb[L * 5 + 40 + (L - 44) // 2] ^= 0x80  # a payload byte of packet 5
+            sb[L * 9 + L - 2] ^= 0x04
+            d = dev(sb)
+            ok = torch.zeros(m, dtype=torch.uint8, device="cuda")
+            engine.verify_strided(d.data_ptr(), L, L, m, ok.data_ptr(), zero_trailer=zero_trailer, stream=stream_handle())
+            torch.cuda.synchronize()
+            w = np.ones(m, np.uint8)
+            w[[5, 9]] = 0
+            np.testing.assert_array_equal(ok.cpu().numpy(), w, err_msg=f"strided L={L}")
+    finally:
+        engine.set_variant(-1)
