@@ -1345,3 +1345,52 @@ def test_verify_residue_row_boundaries(engine, variant, zero_trailer):
             np.testing.assert_array_equal(ok.cpu().numpy(), w, err_msg=f"strided L={L}")
     finally:
         engine.set_variant(-1)
+
+
+def test_large_mixed_mtu_batch_oct_result_flushes(engine, ab_engine):
+    """A C2-shaped batch big enough that every oct wave walks more than kOctRes (8) blocks, so its
+    register-buffered block results are stored from inside the ring as well as after it: the
+    default hybrid launch against the one-packet pipeline (forced variant 16) on every packet and
+    against the oracle on a sample; then trailers written by the default dispatch verify clean,
+    and flipped bits are caught exactly."""
+    import icrc_amd
+
+    n = 3 << 20  # 768 packets per oct wave: 12 blocks
+    w = icrc_amd.workloads.mixed_mtu_stream(n, seed=99)
+    s = stream_handle()
+    d_buf = icrc_amd.workloads.synthesize(engine, w, stream=s)
+    d_off, d_len = dev(w.off), dev(w.lens)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ref = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, out.data_ptr(), stream=s)
+    engine.set_variant(16)
+    try:
+        engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, ref.data_ptr(), stream=s)
+    finally:
+        engine.set_variant(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    rng = np.random.default_rng(3)
+    pick = np.unique(np.concatenate([np.arange(2048), np.arange(n - 2048, n), rng.choice(n, 20000, replace=False)]))
+    lo = w.off[pick].astype(np.int64)
+    span = w.lens[pick].astype(np.int64)
+    idx = np.concatenate([np.arange(a, a + b) for a, b in zip(lo, span)])
+    host = d_buf[torch.from_numpy(idx).cuda()].cpu().numpy()
+    soff = np.zeros(pick.size, np.uint64)
+    soff[1:] = np.cumsum(span[:-1]).astype(np.uint64)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32)[pick], oracle_icrcs(host, soff, w.lens[pick]))
+    # trailers by the default dispatch, then verify through it: clean, then with flipped bits
+    engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, out.data_ptr(), write_trailer=True,
+                         stream=s)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, ok.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert bool((ok == 1).all())
+    bad = rng.choice(n, 500, replace=False)
+    pos = (w.off[bad] + 40 + (w.lens[bad] - 44) // 2).astype(np.int64)
+    d_buf[torch.from_numpy(pos).cuda()] ^= 0x20
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, ok.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    want = np.ones(n, np.uint8)
+    want[bad] = 0
+    np.testing.assert_array_equal(ok.cpu().numpy(), want)
