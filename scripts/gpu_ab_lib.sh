@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of two builds of the library on one box: alternating processes of scripts/ab_variants.py,
 # the B build selected with ICRC_AMD_LIB (default: open-rdma-driver_amd/_build_ab/libicrc_amd_old.so).
-# VARIANTS (default -1,19), REPS (default 3).  Output: gpurun_out/ab_lib.jsonl, one line per
+# VARIANTS (default -1), JOBS (ab_variants.py), REPS (default 3).  Output: gpurun_out/ab_lib.jsonl, one line per
 # (build, workload, variant) per repetition.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
