@@ -69,7 +69,8 @@ extern "C" {
 typedef struct icrc_engine icrc_engine;
 
 /* ---- engine lifetime ------------------------------------------------------------------ */
-/* One engine per GPU: owns the 160 KiB LDS table image in HBM, a stream and staging. */
+/* One engine per GPU: owns the LDS table images in HBM (160 KiB each, plus a 36 KiB compact form the
+ * kernels replicate into LDS), a stream and staging. */
 int icrc_engine_create(int device, icrc_engine **out);
 int icrc_engine_destroy(icrc_engine *engine);
 /* Lazily created, lock-protected default engine for `device` (-1 = current HIP device). */
@@ -364,7 +365,7 @@ void icrc_write_ip_udp_header(uint8_t *buf, uint32_t src_ip, uint16_t src_port, 
 int icrc_rdma_header_len(uint8_t opcode);
 
 /* ---- host-only helpers (no GPU needed) -------------------------------------------------- */
-/* The 160 KiB LDS table image the kernel uploads (layout documented in DESIGN.md). */
+/* The 160 KiB LDS table image the kernels build in LDS (layout documented in DESIGN.md). */
 int icrc_table_image(uint32_t *out_words, uint32_t nwords);
 /* The quad kernel's image (four packets per wavefront): M^16 bulk tables, M^(16 - (l & 15))
  * final tables, same layout. */
