@@ -667,8 +667,9 @@ const char *icrc_version(void) {
 #else
 #define ICRC_BUILD_KIND ""
 #endif
-    return "icrc_amd 0.3 gfx950: wave-per-packet end-aligned column Horner, LDS M^64 byte tables "
-           "(32x bank-replicated) + per-lane M^(64-l) nibble tables, prefetch ring, coalesced results"
+    return "icrc_amd 0.4 gfx950: end-aligned column Horner (one packet per wave for long packets, eight per "
+           "wave in 10-row frames for short ones), LDS byte tables replicated 32x from a 36 KiB compact image + "
+           "per-lane nibble tables, prefetch rings, register-buffered results, verify by CRC-32 residue"
            ICRC_BUILD_KIND;
 #undef ICRC_BUILD_KIND
 }

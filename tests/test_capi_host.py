@@ -394,3 +394,38 @@ def test_rx_parse_oracle_matches_kernel_model():
             if f in ("icrc_ok", "_pad"):
                 continue
             assert np.all(got[f] == want[i][f]), (i, f, got[f], want[i][f])
+
+
+def test_header_is_c99_and_links(tmp_path):
+    """include/icrc.h is the FFI boundary a Rust / C caller binds: it compiles as strict C99 and a C
+    program links against libicrc_amd.so and gets a clean error, not a crash, with no GPU."""
+    import shutil
+    import subprocess
+
+    import icrc_amd
+
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib_dir = os.path.dirname(icrc_amd.LIB_PATH)
+    src = tmp_path / "ffi.c"
+    src.write_text(
+        '#include "icrc.h"\n#include <stdio.h>\n#include <string.h>\n'
+        "int main(void) {\n"
+        "    int err = 0;\n"
+        "    unsigned char pkt[8] = {0};\n"
+        "    (void)icrc_compute(pkt, sizeof pkt, &err);  /* len < 44: an error code, not a panic */\n"
+        "    if (err != ICRC_EINVAL) return 2;\n"
+        "    icrc_engine *e = NULL;\n"
+        "    int rc = icrc_engine_default(-1, &e);\n"
+        '    printf("%d %s\\n", rc, icrc_version());\n'
+        "    return strncmp(icrc_version(), \"icrc_amd\", 8) == 0 ? 0 : 3;\n"
+        "}\n")
+    exe = tmp_path / "ffi"
+    subprocess.run([gcc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(root, "include"),
+                    str(src), "-L", lib_dir, "-licrc_amd", f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    rc = int(out.stdout.split()[0])
+    assert rc in (0, icrc_amd.ENODEV)  # ENODEV here (no GPU); 0 on a GPU box
