@@ -800,6 +800,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 49: (void)launch_oct(MODE, p, grid, s, 9); break;  // diagnostic: set setup by arithmetic (strided only)
     case 50: (void)launch_oct(MODE, p, grid, s, 10); break;  // diagnostic: 49, loads only
     case 51: (void)launch_oct(MODE, p, grid, s, 11); break;  // diagnostic: no raised priority
+    case 52: (void)launch_oct(MODE, p, grid, s, 12); break;  // diagnostic: block preparation reused (strided)
 #endif
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }

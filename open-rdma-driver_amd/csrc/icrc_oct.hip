@@ -309,8 +309,10 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
 // loads).
 // 9 / 10 = the full kernel / the loads-only build with each set's per-lane packet data computed
 // from the index (strided uniform batches only: no ds_bpermute on the path to a frame's loads;
-// wrong on anything else); 11 = the full kernel without the raised wave priority.
-constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11) ? 0 : d; }
+// wrong on anything else); 11 = the full kernel without the raised wave priority; 12 = the full
+// kernel with the per-block preparation (classification, sort, frame schedule) done once per wave
+// and reused (strided batches of uniform full blocks only).
+constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11 || d == 12) ? 0 : d; }
 template <int MODE, bool RAGGED, bool TRAILER, int DIAGX>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
@@ -555,7 +557,14 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                             : static_cast<uint64_t>(lo + q) * p.stride;
                 L = p.len ? m_len : p.ulen;
             }
-            if (oct_block<MODE>(p, NB, off, L, valid, lo, nb_next, lane) != 0) irregular = true;
+            if (DIAGX == 12 && !RAGGED && nb_next > 0 && (nb_next + 1) * 64 <= static_cast<int>(nq)) {
+                // DIAG 12 (strided, full blocks): the first block's preparation reused, only its
+                // position moved (what a free block schedule would leave)
+                NB.block = nb_next;
+                NB.boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(nb_next) * 64u) * p.stride;
+            } else if (oct_block<MODE>(p, NB, off, L, valid, lo, nb_next, lane) != 0) {
+                irregular = true;
+            }
             nb_next += 1;
             nb_ready = NB.nfr > 0;
         }
@@ -683,6 +692,7 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
         case 9: ICRC_O(M, R, false, 9); break;                       \
         case 10: ICRC_O(M, R, false, 10); break;                     \
         case 11: ICRC_O(M, R, false, 11); break;                     \
+        case 12: ICRC_O(M, R, false, 12); break;                     \
         default: ICRC_O(M, R, false, 8); break;                      \
         }                                                            \
     } while (0)

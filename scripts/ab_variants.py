@@ -28,7 +28,7 @@ def main():
     rounds = int(os.environ.get("ROUNDS", "5"))
     launches = int(os.environ.get("LAUNCHES", "10"))
     # the product library (or ICRC_AMD_LIB's build) unless a variant exists only in the A/B build
-    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26) for v in variants if v >= 0)
+    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26, 49, 51, 52) for v in variants if v >= 0)
     eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library() if ab_only else None)
     s = torch.cuda.current_stream().cuda_stream
     jobs = {}

@@ -1117,7 +1117,7 @@ def test_split_batches_concurrent_streams(engine):
     assert not errors, errors
 
 
-DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 141, 146, 148, 241)
+DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 141, 146, 148, 241)
 
 
 def test_kernel_variant_validation(engine, ab_engine):
@@ -1128,7 +1128,7 @@ def test_kernel_variant_validation(engine, ab_engine):
     for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302):
         engine.set_variant(v)
     engine.set_variant(-1)
-    for v in (-2, 1, 10, 14, 23, 27, 36, 52, 99, 100, 116, 152, 303, 400) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
+    for v in (-2, 1, 10, 14, 23, 27, 36, 53, 99, 100, 116, 153, 303, 400) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
         with pytest.raises(icrc_amd.IcrcError) as e:
             engine.set_variant(v)
         assert e.value.rc == icrc_amd.EINVAL, v
