@@ -365,7 +365,10 @@ void icrc_write_ip_udp_header(uint8_t *buf, uint32_t src_ip, uint16_t src_port, 
 int icrc_rdma_header_len(uint8_t opcode);
 
 /* ---- host-only helpers (no GPU needed) -------------------------------------------------- */
-/* The 160 KiB LDS table image the kernels build in LDS (layout documented in DESIGN.md). */
+/* The 160 KiB LDS table image the kernels build in LDS (layout documented in DESIGN.md).  With
+ * nwords >= 40960 + 9216 the buffer also receives the compact form the engine keeps after the
+ * image in HBM and the kernels replicate into LDS: the 1024 distinct bulk entries, then the final
+ * tables. */
 int icrc_table_image(uint32_t *out_words, uint32_t nwords);
 /* The quad kernel's image (four packets per wavefront): M^16 bulk tables, M^(16 - (l & 15))
  * final tables, same layout. */

@@ -1005,18 +1005,21 @@ int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t s
 int icrc_table_image(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image(out_words);
+    if (nwords >= icrc::kTableBufWords) icrc::append_compact_image(out_words);  // the device buffer
     return ICRC_OK;
 }
 
 int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image_quad(out_words);
+    if (nwords >= icrc::kTableBufWords) icrc::append_compact_image(out_words);  // the device buffer
     return ICRC_OK;
 }
 
 int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image_oct(out_words);
+    if (nwords >= icrc::kTableBufWords) icrc::append_compact_image(out_words);  // the device buffer
     return ICRC_OK;
 }
 

@@ -226,10 +226,14 @@ def version() -> str:
     return lib.icrc_version().decode()
 
 
-def table_image(width: int = 64) -> np.ndarray:
+COMPACT_WORDS = 1024 + 8192  # kCompactWords: 1024 bulk entries + the 32 KiB final tables
+
+
+def table_image(width: int = 64, compact: bool = False) -> np.ndarray:
     """The LDS table image the kernels upload for rows of `width` words: 64 (one packet per
-    wavefront), 16 (quad: four packets per wavefront) or 8 (oct: eight)."""
-    img = np.zeros(LDS_WORDS, dtype=np.uint32)
+    wavefront), 16 (quad: four packets per wavefront) or 8 (oct: eight).  compact: followed by
+    the compact form the engine keeps after it in HBM (what the kernels replicate into LDS)."""
+    img = np.zeros(LDS_WORDS + (COMPACT_WORDS if compact else 0), dtype=np.uint32)
     fn = {64: lib.icrc_table_image, 16: lib.icrc_table_image_quad, 8: lib.icrc_table_image_oct}[width]
     _check(fn(img.ctypes.data, img.size), "icrc_table_image")
     return img

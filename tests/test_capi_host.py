@@ -429,3 +429,29 @@ def test_header_is_c99_and_links(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     rc = int(out.stdout.split()[0])
     assert rc in (0, icrc_amd.ENODEV)  # ENODEV here (no GPU); 0 on a GPU box
+
+
+@pytest.mark.parametrize("W", [64, 16, 8])
+def test_compact_table_replicates_to_the_lds_image(W):
+    """The engine keeps a 36 KiB compact form after each 160 KiB image and every workgroup
+    rebuilds the image in LDS from it (table_fill, icrc_device.h): thread t takes bulk entry t =
+    B_b[x] (b = t >> 8, x = t & 255) and stores it into the 32 bank copies at
+    (b >> 1) * 65536 + x * 256 + (b & 1) * 128 (eight 16-byte stores, chunk (k + x) & 7 first),
+    plus 2 x 16 bytes of the final tables.  Emulated here: the result is the full image, word for
+    word."""
+    import icrc_amd
+
+    buf = icrc_amd.table_image(width=W, compact=True)
+    full, comp = buf[:icrc_amd.LDS_WORDS], buf[icrc_amd.LDS_WORDS:]
+    assert comp.size == icrc_amd.COMPACT_WORDS
+    lds = np.full(icrc_amd.LDS_WORDS, 0xDEADBEEF, np.uint32)
+    for t in range(1024):
+        b, x = t >> 8, t & 255
+        row = ((b >> 1) * 65536 + x * 256 + (b & 1) * 128) // 4
+        for k in range(8):
+            c = (k + x) & 7
+            lds[row + 4 * c: row + 4 * c + 4] = comp[t]
+    fin = 131072 // 4
+    lds[fin:] = comp[1024:]
+    np.testing.assert_array_equal(lds, full)
+    assert np.array_equal(icrc_amd.table_image(width=W), full)
