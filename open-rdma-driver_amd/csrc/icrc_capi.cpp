@@ -127,6 +127,12 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>(p.n, 1u), static_cast<uint32_t>(e->num_cu)))
                               : grid_for(e, p.n);
     p.split_len = 0;
+#ifdef ICRC_AB_BUILD  // A/B: the persistent waves' work skew (BatchParams::skew), read per call:
+    // ICRC_AB_SKEW both kernels, ICRC_AB_SKEW_OCT / ICRC_AB_SKEW_LONG one of them
+    if (const char *v = std::getenv("ICRC_AB_SKEW")) p.skew = static_cast<uint32_t>(std::atoi(v)) * 0x10001u;
+    if (const char *v = std::getenv("ICRC_AB_SKEW_OCT")) p.skew = (p.skew & 0xFFFF0000u) | (std::atoi(v) & 0xFFFF);
+    if (const char *v = std::getenv("ICRC_AB_SKEW_LONG")) p.skew = (p.skew & 0xFFFFu) | (static_cast<uint32_t>(std::atoi(v)) << 16);
+#endif
     if (e->variant >= 0 && e->variant < icrc::kHybridVariantBase) {
         p.variant = e->variant;
         return icrc::launch_batch(mode, p, grid, stream);

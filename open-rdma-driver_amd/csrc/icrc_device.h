@@ -44,6 +44,29 @@ __device__ __forceinline__ uint32_t step_m64(const char *lds, uint32_t s, uint32
     return xor3(xor3(u, r0, r1), r2, r3);
 }
 
+// This wave's packets [lo, hi) of a workgroup range of 16 x chunk packets from g0: equal shares,
+// or (skew != 0, chunk a multiple of 64) wave slot k takes 1 + skew (3 - 2 (k >> 2)) / 1024 of
+// the average, in whole units of 8 << (skew >> 12) packets (a multiple of 8 dividing 64), the
+// oldest waves of each SIMD the most (kWaveSkew, icrc_internal.h).
+__device__ __forceinline__ void wave_range(uint64_t g0, uint32_t chunk, uint32_t wave, uint32_t skew, uint64_t &lo,
+                                           uint64_t &hi) {
+    const uint32_t unit = 8u << ((skew >> 12) & 3u);
+    skew &= 0xFFFu;
+    if (skew == 0u || chunk < 64u) {
+        lo = g0 + static_cast<uint64_t>(wave) * chunk;
+        hi = lo + chunk;
+        return;
+    }
+    const uint64_t U = 16u * static_cast<uint64_t>(chunk) / unit;  // the workgroup's units
+    auto start = [&](uint32_t k) __attribute__((always_inline)) -> uint64_t {
+        const int f = static_cast<int>(k >> 2), r = static_cast<int>(k & 3u);
+        const int64_t num = 1024 * static_cast<int64_t>(k) + static_cast<int64_t>(skew) * (4 * f * (4 - f) + r * (3 - 2 * f));
+        return U * static_cast<uint64_t>(num) / (16u * 1024u);
+    };
+    lo = g0 + unit * start(wave);
+    hi = g0 + unit * start(wave + 1u);
+}
+
 __device__ __forceinline__ uint32_t mul_m64(const char *lds, uint32_t s, const LaneConsts &c) {
     return step_m64(lds, s, 0u, c);
 }

@@ -38,6 +38,21 @@ void append_compact_image(uint32_t *img);  // img[kLdsWords ..] <- compact form 
 uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
 
 // ---- kernel launch parameters ------------------------------------------------------------
+// Work skew of a workgroup's persistent waves, in 1/1024: the four waves of a SIMD are served by
+// age (the oldest wins issue arbitration), so with equal shares the oldest finish first and the
+// youngest run the tail alone (diagnostic 53: ends at 200 / 217 / 237 / 260 us on 4 Mi x 316 B,
+// identical run to run).  Wave slot k (age rank a = k / 4) takes a share 1 + e (3 - 2a) / 1024;
+// e for the oct kernel in bits 0-11, for the one-packet pipeline (batch and long-packet
+// workgroups) in bits 16-27; bits 12-13 / 28-29: the shares' unit, 8 << that packets (the oct
+// kernel counts its blocks from its own first packet, so one set will do; the one-packet pipeline
+// keeps 64-packet blocks: whole-line result stores).  Units of one set measured no better than
+// whole blocks (profiles/r03_probe_skew_unit.jsonl), so both keep 64.
+constexpr uint32_t kWaveSkewOct = 45u | (3u << 12);  // probe_skew.py: C2 -3.6 %, 316 B -2 %, 1 KiB -3.4 %
+// The one-packet pipeline: 0.  Its chunks are 4 blocks per wave on C1 and no skew measured better
+// beyond the box noise (profiles/r03_probe_skew_2.jsonl).  (A/B: ICRC_AB_SKEW_OCT / _LONG.)
+constexpr uint32_t kWaveSkewLong = 3u << 12;  // no skew (unit 64)
+constexpr uint32_t kWaveSkew = kWaveSkewOct | (kWaveSkewLong << 16);
+
 struct BatchParams {
     uint8_t *base;
     const uint64_t *off;  // nullptr => strided (offset = i * stride)
@@ -59,6 +74,7 @@ struct BatchParams {
     int long_variant;    // launch_long: 0 = filtered S = 2 pipeline (default), 1 = compacting S = 1 walker
     int spread;          // one-packet pipeline: consecutive waves' packets on different workgroups
                          // (small host-mapped batches: more CUs issue PCIe reads at once)
+    uint32_t skew = kWaveSkew;  // persistent waves' work shares by age (wave_range, icrc_device.h)
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
@@ -77,19 +93,19 @@ constexpr int kRxVariantBase = 300;
 // accepts only result-exact ones: 0, 13, 16, 17 (one packet per wave) and 40 (oct).  The A/B
 // library (built with ICRC_AB_BUILD: _build/libicrc_amd_ab.so, for measurement scripts and the
 // bench's loads-only denominator) adds the quad kernels 20, 24-26 (icrc_quad.hip) and the
-// diagnostics 15, 18, 19, 21, 22, 31, 32, 35, 41-52, whose results are wrong by design (49 and 51 are
+// diagnostics 15, 18, 19, 21, 22, 31, 32, 35, 41-53, whose results are wrong by design (49 and 51 are
 // exact on strided batches only / on all batches, but ablations all the same).
 #ifdef ICRC_AB_BUILD
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 24: case 25: case 26: case 31: case 32: case 35:
-    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51: case 52:
+    case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51: case 52: case 53:
         return true;
     default:
         return false;
     }
 }
-inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 52); }
+inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 53); }
 #else
 inline bool is_batch_variant(int v) { return v == 0 || v == 13 || v == 16 || v == 17 || v == 40; }
 inline bool is_short_variant(int v) { return v == 40; }

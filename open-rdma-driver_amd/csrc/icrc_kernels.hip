@@ -70,9 +70,10 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
         // image is loaded inside run_pipelined<TABLE>, overlapped with the first row loads
         TableShare tv;
         const uint32_t chunk = wave_chunk(p.n, tw);
-        const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+        uint64_t lo64 = static_cast<uint64_t>(gw) * chunk, hi64 = lo64 + chunk;
+        if (!p.spread) wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew >> 16, lo64, hi64);
         const uint32_t lo = lo64 < p.n ? static_cast<uint32_t>(lo64) : p.n;
-        const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+        const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo);
         run_pipelined<MODE, S, D, ABL, 0, false, TRAILER, true>(p, lds, c, lane, lo, nq, &tv);
     }
 }
@@ -801,6 +802,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 50: (void)launch_oct(MODE, p, grid, s, 10); break;  // diagnostic: 49, loads only
     case 51: (void)launch_oct(MODE, p, grid, s, 11); break;  // diagnostic: no raised priority
     case 52: (void)launch_oct(MODE, p, grid, s, 12); break;  // diagnostic: block preparation reused (strided)
+    case 53: (void)launch_oct(MODE, p, grid, s, 13); break;  // diagnostic: per-wave start / end stamps
 #endif
     default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
     }

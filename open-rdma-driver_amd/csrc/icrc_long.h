@@ -753,12 +753,12 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
     const uint32_t tw = nblk * kWavesPerGroup;
-    const uint32_t gw = bid * kWavesPerGroup + wave;
     const uint32_t chunk = wave_chunk(p.n, tw);
-    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    uint64_t lo64, hi64;
+    wave_range(static_cast<uint64_t>(bid) * kWavesPerGroup * chunk, chunk, wave, p.skew >> 16, lo64, hi64);
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
-    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
     if constexpr (COMPACT) {
         run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
     } else {

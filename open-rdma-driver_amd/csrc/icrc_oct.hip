@@ -311,8 +311,9 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
 // from the index (strided uniform batches only: no ds_bpermute on the path to a frame's loads;
 // wrong on anything else); 11 = the full kernel without the raised wave priority; 12 = the full
 // kernel with the per-block preparation (classification, sort, frame schedule) done once per wave
-// and reused (strided batches of uniform full blocks only).
-constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11 || d == 12) ? 0 : d; }
+// and reused (strided batches of uniform full blocks only); 13 = the full kernel, then each wave
+// stamps its start and end (s_memrealtime, 100 MHz) over its first four results (load balance).
+constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11 || d == 12 || d == 13) ? 0 : d; }
 template <int MODE, bool RAGGED, bool TRAILER, int DIAGX>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
@@ -323,6 +324,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
     constexpr int B = 2 * P;
     if (nq == 0) return;
+    const uint64_t t_start = DIAGX == 13 ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int nblocks = static_cast<int>((nq + 63u) >> 6);
     const uint32_t grp = lane >> 3;
     const int col = static_cast<int>(lane & 7u);
@@ -619,6 +621,15 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             }
         }
     }
+    if constexpr (DIAGX == 13 && MODE == kCompute) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const __amdgpu_buffer_rsrc_t os =
+            __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0, 0x00020000);
+        const uint32_t v = lane == 0 ? static_cast<uint32_t>(t_start) : lane == 1 ? static_cast<uint32_t>(t_start >> 32)
+                         : lane == 2 ? static_cast<uint32_t>(t_end) : static_cast<uint32_t>(t_end >> 32);
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_raw_buffer_store_b32(v, os, static_cast<int>(lane < 4u ? lane * 4u : kOctOOR), 0, 0);
+    }
 }
 
 // The oct kernel's work for workgroup `bid` of `nblk` (its own kernel, or the short-packet
@@ -644,11 +655,11 @@ __device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint
     LaneConsts c;
     c.pc = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 16);
     c.fin = kFinalBase + lane * 4u;
-    const uint32_t gw = bid * kWavesPerGroup + wave;
-    const uint64_t lo64 = static_cast<uint64_t>(gw) * chunk;
+    uint64_t lo64, hi64;
+    wave_range(static_cast<uint64_t>(bid) * kWavesPerGroup * chunk, chunk, wave, p.skew & 0xFFFFu, lo64, hi64);
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
-    const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
+    const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
     run_oct<MODE, RAGGED, TRAILER, DIAG>(p, lds, c, lane, lo, nq);
 }
 
@@ -693,6 +704,7 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
         case 10: ICRC_O(M, R, false, 10); break;                     \
         case 11: ICRC_O(M, R, false, 11); break;                     \
         case 12: ICRC_O(M, R, false, 12); break;                     \
+        case 13: ICRC_O(M, R, false, 13); break;                     \
         default: ICRC_O(M, R, false, 8); break;                      \
         }                                                            \
     } while (0)
