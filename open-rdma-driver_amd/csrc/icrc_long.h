@@ -755,7 +755,9 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     const uint32_t tw = nblk * kWavesPerGroup;
     const uint32_t chunk = wave_chunk(p.n, tw);
     uint64_t lo64, hi64;
-    wave_range(static_cast<uint64_t>(bid) * kWavesPerGroup * chunk, chunk, wave, p.skew >> 16, lo64, hi64);
+    // equal shares: in the hybrid launch these workgroups fill CUs as the oct ones retire, and a
+    // skew measured slower on C2 (profiles/r03_probe_skew_long.jsonl)
+    wave_range(static_cast<uint64_t>(bid) * kWavesPerGroup * chunk, chunk, wave, 0u, lo64, hi64);
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);

@@ -25,6 +25,17 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     jobs, keep = {}, []
     for name in os.environ.get("JOBS", "C1,C2,S316,C2k").split(","):
+        if name == "C1v":  # verify (is_icrc_valid) of C1, trailers written first
+            w = workloads.write_middle_stream(1 << 20)
+            L = int(w.lens[0])
+            b = workloads.synthesize(eng, w, stream=s)
+            scratch = torch.zeros(w.n, dtype=torch.int32, device="cuda")
+            eng.compute_strided(b.data_ptr(), L, L, w.n, scratch.data_ptr(), True, s)
+            ok = torch.zeros(w.n, dtype=torch.uint8, device="cuda")
+            keep += [b, scratch, ok]
+            jobs[name] = (lambda b=b, ok=ok, n=w.n, L=L: eng.verify_strided(b.data_ptr(), L, L, n, ok.data_ptr(), False, s),
+                          w.n * L, ok)
+            continue
         if name in ("C1", "S316"):
             w = workloads.write_middle_stream(1 << 22, pmtu=256) if name == "S316" else workloads.write_middle_stream(1 << 20)
             L = int(w.lens[0])
