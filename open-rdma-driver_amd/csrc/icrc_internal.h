@@ -46,11 +46,13 @@ uint32_t advance_words(uint32_t state, uint32_t nwords);  // M^nwords(state)
 // workgroups) in bits 16-27; bits 12-13 / 28-29: the shares' unit, 8 << that packets (the oct
 // kernel counts its blocks from its own first packet, so one set will do; the one-packet pipeline
 // keeps 64-packet blocks: whole-line result stores).  Units of one set measured no better than
-// whole blocks (profiles/r03_probe_skew_unit.jsonl), so both keep 64.
+// whole blocks for the oct kernel (profiles/r03_probe_skew_unit.jsonl).
 constexpr uint32_t kWaveSkewOct = 45u | (3u << 12);  // probe_skew.py: C2 -3.6 %, 316 B -2 %, 1 KiB -3.4 %
-// The one-packet pipeline: 0.  Its chunks are 4 blocks per wave on C1 and no skew measured better
-// beyond the box noise (profiles/r03_probe_skew_2.jsonl).  (A/B: ICRC_AB_SKEW_OCT / _LONG.)
-constexpr uint32_t kWaveSkewLong = 3u << 12;  // no skew (unit 64)
+// The batch kernel's one-packet pipeline (C1: 4 blocks per wave, too coarse for whole-block
+// shares; units of 8 packets): e = 180, C1 -2.9 %, C1 verify -2 % (profiles/r03_probe_skew_long.jsonl).
+// The hybrid launch's long-packet workgroups keep equal shares (long_body).  (A/B:
+// ICRC_AB_SKEW_OCT / ICRC_AB_SKEW_LONG.)
+constexpr uint32_t kWaveSkewLong = 180u;
 constexpr uint32_t kWaveSkew = kWaveSkewOct | (kWaveSkewLong << 16);
 
 struct BatchParams {
