@@ -71,8 +71,14 @@ def parse(argv=None):
     ap.add_argument("--extra", action="store_true",
                     help="also time verify, trailer stores, mixed-MTU, 16 MiB round trip, packetizer, receive "
                          "parse and the host-resident path")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds: process-group init and every collective / barrier (N > 1)")
+    ap.add_argument("--launch-timeout", type=float, default=540.0,
+                    help="seconds: the launcher kills the whole rank group and exits 3 when the ranks have not "
+                         "finished by then (N > 1)")
     ap.add_argument("--cpu-stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--inject-fault-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -116,8 +122,37 @@ def launch_ranks(args, argv) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    # a collective that outlives --dist-timeout raises on its rank instead of blocking forever
+    env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     log("bench.py: launching " + " ".join(cmd[1:]))
-    return subprocess.run(cmd, env=env).returncode
+    # its own session: on expiry the whole group (torchrun + every rank) is killed, never re-exec'd
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return p.wait(timeout=args.launch_timeout)
+    except subprocess.TimeoutExpired:
+        import signal
+
+        for sig, grace in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        log(f"bench.py: the {args.gpus} ranks did not finish within --launch-timeout {args.launch_timeout:g} s; "
+            "killed their process group")
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": args.gpus,
+                          "error": f"ranks timed out after {args.launch_timeout:g} s (killed)"}), flush=True)
+        return 3
+
+
+def _dist_timeout(args):
+    from datetime import timedelta
+
+    return timedelta(seconds=args.dist_timeout)
 
 
 # ---- timing --------------------------------------------------------------------------------
@@ -192,7 +227,7 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         return 2
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=_dist_timeout(args))
     import icrc_amd
     from icrc_amd import shard, workloads
 
@@ -716,7 +751,9 @@ def run_cpu_stub(args, rank: int, world: int) -> int:
     from icrc_amd import shard
 
     if world > 1:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=_dist_timeout(args))
+    if rank == args.stall_rank:  # tests: a rank that never reaches the first barrier
+        time.sleep(3600)
     L = 28 + 28 + args.pmtu + 4
     if args.scaling == "weak":  # one stream per rank
         lo, hi, key = 0, args.packets, 0x5EED5EED + rank

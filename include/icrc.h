@@ -263,8 +263,11 @@ typedef struct icrc_write_msg {
     uint64_t payload_offset; /* byte offset of the message payload in d_src */
     uint64_t out_offset;     /* byte offset of packet 0 in d_wire */
     uint32_t total_len;      /* sge.len: bytes to send, drives segmentation (read requests: the
-                                secondary RETH len) */
-    uint32_t reth_len;       /* common.total_len: the RETH len of every packet (common.rs:113) */
+                                secondary RETH len; ICRC_WRITE_RUST_DRIVER: the SG list's total
+                                length, sg_list.get_total_length(), logic.rs:207) */
+    uint32_t reth_len;       /* common.total_len: the RETH len of every packet (common.rs:113);
+                                ICRC_WRITE_RUST_DRIVER: only FIRST packets carry it (logic.rs:121-125,
+                                224-228), the others their own lengths (240, 265) */
     uint32_t pmtu;           /* 256 .. 4096 (WRITE / READ RESPONSE) */
     uint32_t rkey;
     uint32_t dqpn;
@@ -280,7 +283,9 @@ typedef struct icrc_write_msg {
     uint8_t flags;           /* ICRC_WRITE_* below */
     uint8_t _pad;
     uint32_t lkey;           /* read requests: the secondary RETH rkey (sge.local_key) */
-} icrc_write_msg; /* 88 bytes */
+    uint32_t imm;            /* ImmDt of a WRITE_WITH_IMM descriptor (ICRC_WRITE_WITH_IMM) */
+    uint32_t _rsvd;          /* 0 */
+} icrc_write_msg; /* 96 bytes */
 #define ICRC_MSG_WRITE 0u         /* Write::handle (write.rs:31-96): WRITE FIRST/MIDDLE/LAST/ONLY  */
 #define ICRC_MSG_READ_RESPONSE 1u /* ReadResponse::handle (read_response.rs:30-95)                 */
 #define ICRC_MSG_READ_REQUEST 2u  /* Read::handle (read.rs:33-89): one 76-byte packet, opcode 0x0C,
@@ -290,9 +295,25 @@ typedef struct icrc_write_msg {
  * builds the frame, net_agent.rs:93; calculate_ipv4_checksum, responser.rs:321-338).  The
  * ICRC masks those bytes, so it is the same either way.  Default: 0, as PacketWriter leaves it. */
 #define ICRC_WRITE_FILL_IPV4_CSUM 0x01u
-/* Segment on the remote VA (rust_driver: calculate_packet_cnt / get_first_packet_max_length,
- * rust_driver/src/utils.rs:19-33) instead of the local VA (emulator, common.rs:152-176). */
-#define ICRC_WRITE_SEG_BY_REMOTE_VA 0x02u
+/* The rust_driver software device's send rule, BlueRDMALogic::send (rust_driver/src/device/software/
+ * logic.rs:109-134, 168-271) instead of the emulator's (write.rs:31-96):
+ *   - segmentation on the REMOTE VA: first packet = pmtu - remote_va % pmtu (get_first_packet_max_length,
+ *     rust_driver/src/utils.rs:19-25); npackets = calculate_packet_cnt (utils.rs:28-33), which
+ *     icrc_write_segment_count(remote_va, total_len, pmtu) returns;
+ *   - opcodes from the descriptor's is_first / is_last (ToCardWriteDescriptor, types.rs:557-609): a
+ *     continuation descriptor (ICRC_WRITE_NOT_FIRST) starts with MIDDLE, one that is not the message's
+ *     end (ICRC_WRITE_NOT_LAST) ends with MIDDLE; a one-packet descriptor takes ONLY / FIRST / LAST
+ *     (write_only_opcode_with_imm: neither flag set -> ONLY, NOT_LAST -> FIRST, otherwise LAST);
+ *   - RETH len: reth_len (common.total_len) on a FIRST packet, the packet's own payload length on a
+ *     one-packet or first continuation packet (:121-125, :224-228), pmtu on MIDDLE (:240), the remaining
+ *     length on the last packet (:265); RETH va = remote_va + bytes before the packet (:229, 244, 264);
+ *   - ICRC_WRITE_WITH_IMM (kind WRITE): LAST / ONLY become WRITE_LAST / WRITE_ONLY_WITH_IMMEDIATE (0x09 /
+ *     0x0B) carrying ImmDt = imm after the RETH (RdmaHeaderReqBthRethImm, packet.rs:354-390);
+ *   - ack_req and solicited are clear on every packet (RdmaMessageMetaCommon, logic.rs:175-186);
+ *     ICRC_WRITE_ACK_REQ / _SOLICITED still set them when given.
+ * PSN +1 per packet (24-bit wrap, Psn::wrapping_add, types.rs:180-183), as in both variants. */
+#define ICRC_WRITE_RUST_DRIVER 0x02u
+#define ICRC_WRITE_SEG_BY_REMOTE_VA ICRC_WRITE_RUST_DRIVER /* the round-1..3 name */
 /* RdmaMessageMetaCommon::solicited on every packet of the message (BTH byte 1 bit 7, packet.rs:
  * 104-110); the emulator's own send paths leave it false (common.rs:90, read.rs:47). */
 #define ICRC_WRITE_SOLICITED 0x04u
@@ -304,6 +325,11 @@ typedef struct icrc_write_msg {
  * is the same (it covers the masked IPv4 / UDP header, which is not stored); d_pkt_len reports
  * L - 28, the bytes written. */
 #define ICRC_WRITE_UDP_PAYLOAD_ONLY 0x10u
+/* ICRC_WRITE_RUST_DRIVER descriptor flags (ToCardWriteDescriptor, types.rs:548-555; ignored otherwise):
+ * is_first = false, is_last = false, and a WriteWithImm descriptor's imm (types.rs:641-648). */
+#define ICRC_WRITE_NOT_FIRST 0x20u
+#define ICRC_WRITE_NOT_LAST 0x40u
+#define ICRC_WRITE_WITH_IMM 0x80u
 /* Number of packets generate_segments_from_request yields (common.rs:152-176) for a message
  * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_SEG_BY_REMOTE_VA);
  * 0 if pmtu == 0. */

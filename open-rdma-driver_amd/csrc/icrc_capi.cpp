@@ -46,28 +46,42 @@ struct SubmitReq {
     uint32_t n;
     uint32_t *res;          // n ICRCs (host memory of the caller)
     int rc = ICRC_OK;
-    bool done = false;
+    bool taken = false;     // in a launch (by this caller or another leader)
+    bool done = false;      // results handed out
+};
+
+// One launch lane of the submitter: a stream and the mapped (offset, length, result) arrays of the
+// launch it carries.  A lane is busy from the moment a leader takes it until the leader has handed
+// out its results.
+struct Lane {
+    hipStream_t stream = nullptr;
+    uint64_t *h_off = nullptr;  // pinned + mapped: packet offsets from the batch base
+    uint32_t *h_len = nullptr;
+    uint32_t *h_res = nullptr;
+    uint64_t *d_off = nullptr;  // their device views
+    uint32_t *d_len = nullptr;
+    uint32_t *d_res = nullptr;
+    bool busy = false;
 };
 
 // The combining submitter: concurrent calls (the emulator's send, packet-handler and receive
-// threads, packet_processor.rs:260 / udp_agent.rs:99) queue here; whichever caller finds no launch
-// in flight takes the queued calls (up to kCap packets) and runs them as ONE compute launch (the
-// others wait on the condition variable), then hands out the results.  Packets are read by the
-// kernel straight from pinned, device-mapped host memory (no copy engine); results come back
-// through mapped pinned memory.
+// threads, packet_processor.rs:260 / udp_agent.rs:99) queue here.  A caller whose call is still
+// queued and who finds a free lane becomes that lane's leader: it takes the queued calls (up to cap
+// packets), runs them as ONE compute launch on the lane's stream and waits for it on that stream
+// alone, then hands out the results.  With kLanes lanes, up to kLanes launches are in flight at once
+// (the emulator's three threads each get a lane; more callers than lanes combine into the next
+// launch).  Packets are read by the kernel straight from pinned, device-mapped host memory (no copy
+// engine); results come back through mapped pinned memory.
 struct Combiner {
+    static constexpr int kLanes = 4;          // <= GPU_MAX_HW_QUEUES (4): one hardware queue each
+    static constexpr uint32_t kCap = 4096;    // array capacity per lane
     std::mutex mu;
     std::condition_variable cv;
     std::vector<SubmitReq *> pending;
-    bool busy = false;
-    hipStream_t stream = nullptr;
-    static constexpr uint32_t kCap = 4096;  // packets per launch (#CUs x 16: one per wave)
-    uint64_t *h_off = nullptr;             // pinned + mapped: packet offsets from the batch base
-    uint32_t *h_len = nullptr;
-    uint32_t *h_res = nullptr;
-    uint64_t *d_off = nullptr;             // their device views
-    uint32_t *d_len = nullptr;
-    uint32_t *d_res = nullptr;
+    Lane lanes[kLanes];
+    uint32_t cap = kCap;  // packets per launch: min(kCap, #CUs x 16) keeps every launch on the one-packet
+                          // pipeline, whose loads stay inside each packet (callers' buffers are unrelated
+                          // host allocations; the oct kernel reads a short packet's rows up to its block end)
 };
 
 }  // namespace
@@ -440,6 +454,7 @@ constexpr size_t kScalarSlotBytes = 65536 + 64;  // any packet the C-ABI accepts
 // threads): one message of the emulator's (configs[0]: 64 x 4156 B) is far below it.  Larger
 // batches take the staged, pipelined H2D path (host_batch).
 constexpr uint32_t kMsgMaxPackets = 1024;
+static_assert(kMsgMaxPackets <= Combiner::kCap, "a message must fit one lane's arrays");
 constexpr size_t kMsgMaxBytes = size_t(8) << 20;
 thread_local StageSlot t_slot;
 
@@ -465,83 +480,86 @@ int stage_slot(const icrc_engine *e, size_t bytes, uint8_t **h, uint8_t **d) {
     return ICRC_OK;
 }
 
-void combiner_release(Combiner &c) {
-    if (c.stream) {
-        (void)hipStreamSynchronize(c.stream);
-        (void)hipStreamDestroy(c.stream);
-        c.stream = nullptr;
+void lane_release(Lane &l) {
+    if (l.stream) {
+        (void)hipStreamSynchronize(l.stream);
+        (void)hipStreamDestroy(l.stream);
     }
-    for (void *p : {static_cast<void *>(c.h_off), static_cast<void *>(c.h_len), static_cast<void *>(c.h_res)})
+    for (void *p : {static_cast<void *>(l.h_off), static_cast<void *>(l.h_len), static_cast<void *>(l.h_res)})
         if (p) (void)hipHostFree(p);
-    c.h_off = nullptr;
-    c.h_len = nullptr;
-    c.h_res = nullptr;
+    l = Lane{};
+}
+
+int lane_init(Lane &l) {
+    void *a = nullptr, *b = nullptr, *r = nullptr, *da = nullptr, *db = nullptr, *dr = nullptr;
+    if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess) {
+        l.stream = nullptr;
+        return ICRC_EDEVICE;
+    }
+    if (hipHostMalloc(&a, Combiner::kCap * 8, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
+    l.h_off = static_cast<uint64_t *>(a);
+    if (hipHostMalloc(&b, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
+    l.h_len = static_cast<uint32_t *>(b);
+    if (hipHostMalloc(&r, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
+    l.h_res = static_cast<uint32_t *>(r);
+    if (hipHostGetDevicePointer(&da, a, 0) != hipSuccess || hipHostGetDevicePointer(&db, b, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&dr, r, 0) != hipSuccess)
+        return ICRC_EDEVICE;
+    l.d_off = static_cast<uint64_t *>(da);
+    l.d_len = static_cast<uint32_t *>(db);
+    l.d_res = static_cast<uint32_t *>(dr);
+    return ICRC_OK;
 }
 
 Combiner *combiner(icrc_engine *e, int *rc) {
     std::lock_guard<std::mutex> lk(e->comb_init_mu);
     if (e->comb) return e->comb.get();
     auto c = std::make_unique<Combiner>();
-    *rc = ICRC_EDEVICE;
-    void *a = nullptr, *b = nullptr, *r = nullptr;
-    void *da = nullptr, *db = nullptr, *dr = nullptr;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        c->stream = nullptr;
-    } else if (hipHostMalloc(&a, Combiner::kCap * 8, hipHostMallocMapped) != hipSuccess ||
-               (c->h_off = static_cast<uint64_t *>(a), false) ||
-               hipHostMalloc(&b, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess ||
-               (c->h_len = static_cast<uint32_t *>(b), false) ||
-               hipHostMalloc(&r, Combiner::kCap * 4, hipHostMallocMapped) != hipSuccess) {
-        *rc = ICRC_ENOMEM;
-    } else {
-        c->h_res = static_cast<uint32_t *>(r);
-        if (hipHostGetDevicePointer(&da, a, 0) == hipSuccess && hipHostGetDevicePointer(&db, b, 0) == hipSuccess &&
-            hipHostGetDevicePointer(&dr, r, 0) == hipSuccess) {
-            c->d_off = static_cast<uint64_t *>(da);
-            c->d_len = static_cast<uint32_t *>(db);
-            c->d_res = static_cast<uint32_t *>(dr);
-            *rc = ICRC_OK;
-            e->comb = std::move(c);
-            return e->comb.get();
+    c->cap = std::min<uint32_t>(Combiner::kCap, static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup);
+    for (Lane &l : c->lanes) {
+        if ((*rc = lane_init(l)) != ICRC_OK) {
+            for (Lane &x : c->lanes) lane_release(x);  // a failed set-up leaves nothing behind; the next call retries
+            return nullptr;
         }
     }
-    combiner_release(*c);  // a failed set-up leaves nothing behind; the next call retries
-    return nullptr;
+    *rc = ICRC_OK;
+    e->comb = std::move(c);
+    return e->comb.get();
 }
 
 void combiner_free(icrc_engine *e) {
     if (!e->comb) return;
-    combiner_release(*e->comb);
+    for (Lane &l : e->comb->lanes) lane_release(l);
     e->comb.reset();
 }
 
-// One compute launch over the taken calls (leader only, outside the combiner lock).
-void run_combined(icrc_engine *e, Combiner &c, SubmitReq *const *reqs, uint32_t nreq) {
+// One compute launch over the taken calls on lane l (its leader only, outside the combiner lock).
+void run_combined(icrc_engine *e, Lane &l, SubmitReq *const *reqs, uint32_t nreq) {
     uintptr_t lo = UINTPTR_MAX;
     for (uint32_t i = 0; i < nreq; i++) lo = std::min(lo, reinterpret_cast<uintptr_t>(reqs[i]->dbase));
     uint32_t k = 0;
     for (uint32_t i = 0; i < nreq; i++) {
         const uint64_t rel = reinterpret_cast<uintptr_t>(reqs[i]->dbase) - lo;
         for (uint32_t q = 0; q < reqs[i]->n; q++, k++) {
-            c.h_off[k] = rel + reqs[i]->off[q];
-            c.h_len[k] = reqs[i]->len[q];
+            l.h_off[k] = rel + reqs[i]->off[q];
+            l.h_len[k] = reqs[i]->len[q];
         }
     }
     BatchParams p{};
     p.base = reinterpret_cast<uint8_t *>(lo);
-    p.off = c.d_off;
-    p.len = c.d_len;
+    p.off = l.d_off;
+    p.len = l.d_len;
     p.n = k;
     // A message of equal, evenly spaced packets (a WRITE's full-MTU segments, one scalar packet)
     // launches as a strided batch: the kernel computes each offset instead of fetching the
     // (offset, length) arrays from host memory first (one PCIe round trip less per call).
-    const uint32_t L0 = c.h_len[0];
-    const uint64_t st = k > 1 ? c.h_off[1] - c.h_off[0] : L0;
-    bool uniform = k > 0 && c.h_off[1 % k] >= c.h_off[0] && st >= L0 && ((lo + c.h_off[0]) & 3u) == 0 &&
+    const uint32_t L0 = l.h_len[0];
+    const uint64_t st = k > 1 ? l.h_off[1] - l.h_off[0] : L0;
+    bool uniform = k > 0 && l.h_off[1 % k] >= l.h_off[0] && st >= L0 && ((lo + l.h_off[0]) & 3u) == 0 &&
                    ((st | L0) & 3u) == 0;
-    for (uint32_t i = 1; uniform && i < k; i++) uniform = c.h_len[i] == L0 && c.h_off[i] == c.h_off[0] + i * st;
+    for (uint32_t i = 1; uniform && i < k; i++) uniform = l.h_len[i] == L0 && l.h_off[i] == l.h_off[0] + i * st;
     if (uniform) {
-        p.base += c.h_off[0];
+        p.base += l.h_off[0];
         p.off = nullptr;
         p.len = nullptr;
         p.stride = st;
@@ -550,14 +568,14 @@ void run_combined(icrc_engine *e, Combiner &c, SubmitReq *const *reqs, uint32_t 
     p.table = e->d_table;
     p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
-    p.out = c.d_res;
-    p.spread = k <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup ? 1 : 0;
-    int rc = dispatch(e, icrc::kCompute, p, c.stream);
-    if (rc == ICRC_OK && hipStreamSynchronize(c.stream) != hipSuccess) rc = ICRC_EDEVICE;
+    p.out = l.d_res;
+    p.spread = 1;  // k <= cap <= #CUs x 16: one workgroup per packet up to #CUs, on the one-packet pipeline
+    int rc = dispatch(e, icrc::kCompute, p, l.stream);
+    if (rc == ICRC_OK && hipStreamSynchronize(l.stream) != hipSuccess) rc = ICRC_EDEVICE;
     k = 0;
     for (uint32_t i = 0; i < nreq; i++) {
         reqs[i]->rc = rc;
-        std::memcpy(reqs[i]->res, c.h_res + k, reqs[i]->n * sizeof(uint32_t));
+        std::memcpy(reqs[i]->res, l.h_res + k, reqs[i]->n * sizeof(uint32_t));
         k += reqs[i]->n;
     }
 }
@@ -566,18 +584,26 @@ int submit(icrc_engine *e, Combiner *c, SubmitReq &req) {
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&req);
     while (!req.done) {
-        if (!c->busy) {  // become the leader: take queued calls up to kCap packets, launch, hand out results
-            c->busy = true;
+        Lane *lane = nullptr;
+        if (!req.taken)
+            for (Lane &l : c->lanes)
+                if (!l.busy) {
+                    lane = &l;
+                    break;
+                }
+        if (lane) {  // become this lane's leader: take queued calls up to cap packets, launch, hand out results
+            lane->busy = true;
             uint32_t take = 0, pk = 0;
-            while (take < c->pending.size() && (take == 0 || pk + c->pending[take]->n <= Combiner::kCap))
+            while (take < c->pending.size() && (take == 0 || pk + c->pending[take]->n <= c->cap))
                 pk += c->pending[take++]->n;
             std::vector<SubmitReq *> batch(c->pending.begin(), c->pending.begin() + take);
             c->pending.erase(c->pending.begin(), c->pending.begin() + take);
+            for (SubmitReq *r : batch) r->taken = true;
             lk.unlock();
-            run_combined(e, *c, batch.data(), take);
+            run_combined(e, *lane, batch.data(), take);
             lk.lock();
             for (SubmitReq *r : batch) r->done = true;
-            c->busy = false;
+            lane->busy = false;
             c->cv.notify_all();
         } else {
             c->cv.wait(lk);
@@ -603,17 +629,25 @@ int scalar_call(const uint8_t *pkt, size_t len, uint32_t *result) {
     return submit(e, c, req);
 }
 
-// Device view of [base + smin, base + smax) when the caller's buffer is pinned host memory
-// (hipHostMalloc / hipHostRegister) covering the whole span, else nullptr.
+// Device view of [base + smin, base + smax) when that whole span lies inside ONE pinned host
+// allocation (hipHostMalloc / hipHostRegister), else nullptr (the caller stages the packets).
 const uint8_t *pinned_device_view(uint8_t *base, uint64_t smin, uint64_t smax) {
-    if (!host_pinned(base + smin) || !host_pinned(base + smax - 1)) return nullptr;
-    void *d0 = nullptr, *d1 = nullptr;
-    if (hipHostGetDevicePointer(&d0, base + smin, 0) != hipSuccess ||
-        hipHostGetDevicePointer(&d1, base + smax - 1, 0) != hipSuccess) {
+    if (!host_pinned(base + smin)) return nullptr;
+    void *d0 = nullptr;
+    if (hipHostGetDevicePointer(&d0, base + smin, 0) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    if (static_cast<uint8_t *>(d1) - static_cast<uint8_t *>(d0) != static_cast<ptrdiff_t>(smax - 1 - smin)) return nullptr;
+    // the allocation holding the first byte must also hold the last one: both ends being pinned is
+    // not enough (pageable memory may lie between two pinned allocations)
+    hipDeviceptr_t abase = nullptr;
+    size_t asize = 0;
+    if (hipMemGetAddressRange(&abase, &asize, d0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(abase), p0 = reinterpret_cast<uintptr_t>(d0);
+    if (p0 < a0 || p0 - a0 + (smax - smin) > asize) return nullptr;
     return static_cast<const uint8_t *>(d0);
 }
 
@@ -637,11 +671,18 @@ int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, 
     int rc = ICRC_OK;
     Combiner *c = combiner(e, &rc);
     if (!c) return rc;
+    if (n > c->cap) return 1;  // a device with fewer than 64 CUs: more packets than one launch takes
     thread_local std::vector<uint64_t> t_off;
     thread_local std::vector<uint32_t> t_res;
     t_off.resize(n);
     t_res.resize(n);
-    const uint8_t *dbase = (smax - smin) <= packed + packed / 4 + 4096 ? pinned_device_view(base, smin, smax) : nullptr;
+    // zero-copy only for a compact span of 4-byte aligned packets: a misaligned one would take the
+    // kernel's byte-wise path over PCIe, slower than packing it into the staging slot
+    bool aligned = true;
+    for (uint32_t i = 0; aligned && i < n; i++)
+        aligned = ((reinterpret_cast<uintptr_t>(base) + off[i]) & 3u) == 0 && (len[i] & 3u) == 0;
+    const uint8_t *dbase =
+        aligned && (smax - smin) <= packed + packed / 4 + 4096 ? pinned_device_view(base, smin, smax) : nullptr;
     if (dbase) {
         for (uint32_t i = 0; i < n; i++) t_off[i] = off[i] - smin;
     } else {

@@ -219,13 +219,14 @@ __global__ __launch_bounds__(256) void icrc_rx_desc_kernel(BatchParams p) {
 enum : int {
     kMLocalVa = 0, kMRemoteVa = 2, kMPayloadOff = 4, kMOutOff = 6, kMTotal = 8, kMRethLen = 9, kMPmtu = 10,
     kMRkey = 11, kMDqpn = 12, kMPsn = 13, kMSrcIp = 14, kMDstIp = 15, kMFirst = 16, kMNpk = 17, kMSlot = 18,
-    kMMsnId = 19, kMKind = 20, kMLkey = 21, kMsgDwords = 22
+    kMMsnId = 19, kMKind = 20, kMLkey = 21, kMImm = 22, kMsgDwords = 24
 };
 static_assert(sizeof(icrc_write_msg) == 4 * kMsgDwords, "icrc_write_msg layout");
 static_assert(offsetof(icrc_write_msg, lkey) == 4 * kMLkey, "icrc_write_msg layout");
+static_assert(offsetof(icrc_write_msg, imm) == 4 * kMImm, "icrc_write_msg layout");
 constexpr uint32_t kSendOOR = 0x80000000u;
 
-struct MsgRegs {  // the 88-byte icrc_write_msg in scalar registers (uniform)
+struct MsgRegs {  // the 96-byte icrc_write_msg in scalar registers (uniform)
     uint32_t s[kMsgDwords];
     int idx;  // message index held, -1 = none
 };
@@ -265,7 +266,10 @@ struct SendPlan {
     uint64_t out;   // packet offset in d_wire
     uint32_t start; // payload byte offset of the segment within the message
     uint32_t plen;  // payload bytes
-    uint32_t hw;    // header words: 14 (IPv4 + UDP + BTH + RETH) or 18 (+ secondary RETH)
+    uint32_t hw;    // header words: 14 (IPv4 + UDP + BTH + RETH), 15 (+ ImmDt) or 18 (+ secondary RETH)
+    uint32_t op;    // BTH opcode
+    uint32_t ack;   // BTH ack_req
+    uint32_t rlen;  // RETH len
     uint32_t L;     // wire length: 4 hw + plen + pad + 4
     uint32_t skip;  // leading packet bytes not stored: 28 under ICRC_WRITE_UDP_PAYLOAD_ONLY, else 0
     int k0;         // stream word index of lane 0 in ring row 0 (rows aligned to kRows)
@@ -278,9 +282,55 @@ __device__ __forceinline__ void plan_empty(SendPlan &g) {
     g.src = g.out = 0;
     g.start = g.plen = g.L = g.skip = 0;
     g.hw = 14;
+    g.op = g.ack = g.rlen = 0;
     g.k0 = 0;
     g.pk = 0xFFFFFFFFu;
     g.fits = g.fast = false;
+}
+
+// Opcode, ack_req, RETH len and header words of packet s of a message (wave-uniform).
+//   emulator (default): Write::handle (write.rs:41-90) / ReadResponse::handle (read_response.rs:30-95):
+//     ONLY / FIRST / MIDDLE / LAST by position, ack_req on LAST / ONLY, RETH len = common.total_len on
+//     every packet (send_write_message, common.rs:113);
+//   ICRC_WRITE_RUST_DRIVER: BlueRDMALogic::send (rust_driver/src/device/software/logic.rs:109-134,
+//     191-271) with the descriptor's is_first / is_last / imm (types.rs:557-609): see include/icrc.h.
+//     RETH len is common.total_len on a FIRST packet and the packet's own payload length otherwise
+//     (first_packet_length :227, pmtu on MIDDLE :240 — a MIDDLE packet carries pmtu bytes — cur_len :265,
+//     sg_list.get_total_length() :124);
+//   READ REQUEST: Read::handle (read.rs:33-89), one packet, RETH + secondary RETH.
+__device__ __forceinline__ void send_opcode(const MsgRegs &m, uint32_t s, SendPlan &g) {
+    const uint32_t kind = msg_kind(m), flags = msg_flags(m), n = msg_u32(m, kMNpk);
+    if (kind == 2u) {
+        g.op = 0x0Cu;
+        g.ack = (flags & ICRC_WRITE_ACK_REQ) ? 1u : 0u;  // the request is signaled (read.rs:37)
+        g.rlen = msg_u32(m, kMRethLen);
+        g.hw = 18;
+        return;
+    }
+    const bool resp = kind == 1u, only = n == 1u, last = s + 1u == n;
+    const uint32_t FIRST = resp ? 0x0Du : 0x06u, MIDDLE = resp ? 0x0Eu : 0x07u, ONLY = resp ? 0x10u : 0x0Au;
+    if (!(flags & ICRC_WRITE_RUST_DRIVER)) {
+        const uint32_t LAST = resp ? 0x0Fu : 0x08u;
+        g.op = only ? ONLY : (s == 0u ? FIRST : (last ? LAST : MIDDLE));
+        g.ack = (only || last) ? 1u : 0u;
+        g.rlen = msg_u32(m, kMRethLen);
+        g.hw = 14;
+        return;
+    }
+    const bool df = !(flags & ICRC_WRITE_NOT_FIRST), dl = !(flags & ICRC_WRITE_NOT_LAST);
+    const bool imm = !resp && (flags & ICRC_WRITE_WITH_IMM);
+    const uint32_t LAST = resp ? 0x0Fu : (imm ? 0x09u : 0x08u);
+    if (only)  // write_only_opcode_with_imm (types.rs:558-581): is_first && is_last -> ONLY, is_first -> FIRST, else LAST
+        g.op = (df && dl) ? (imm ? 0x0Bu : ONLY) : (df ? FIRST : LAST);
+    else if (s == 0u)  // write_first_opcode (types.rs:583-590)
+        g.op = df ? FIRST : MIDDLE;
+    else if (!last)  // write_middle_opcode (types.rs:592-598)
+        g.op = MIDDLE;
+    else  // write_last_opcode_with_imm (types.rs:600-609)
+        g.op = dl ? LAST : MIDDLE;
+    g.ack = (flags & ICRC_WRITE_ACK_REQ) ? 1u : 0u;  // ack_req: false (logic.rs:184)
+    g.rlen = (g.op == FIRST) ? msg_u32(m, kMRethLen) : g.plen;
+    g.hw = (g.op == 0x09u || g.op == 0x0Bu) ? 15u : 14u;  // + ImmDt (RdmaHeaderReqBthRethImm, packet.rs:354-360)
 }
 
 __device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const uint8_t *src, uint64_t src_bytes,
@@ -289,11 +339,11 @@ __device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const
     g.pk = pk;
     const uint32_t s = pk - msg_u32(m, kMFirst);
     const uint32_t kind = msg_kind(m), pmtu = msg_u32(m, kMPmtu), total = msg_u32(m, kMTotal);
-    if (kind == 2u) {  // READ REQUEST: one packet, no payload, a second RETH (read.rs:57-74)
-        g.hw = 18;
-    } else {
+    if (kind != 2u) {  // a READ REQUEST is one packet with no payload (read.rs:57-74)
         if (kind > 2u || pmtu == 0u) return;
-        const bool by_remote = (msg_flags(m) & ICRC_WRITE_SEG_BY_REMOTE_VA) != 0u;
+        // segmentation VA: the local VA (generate_segments_from_request, common.rs:152-176) or, for
+        // rust_driver, the remote VA (get_first_packet_max_length, utils.rs:19-25)
+        const bool by_remote = (msg_flags(m) & ICRC_WRITE_RUST_DRIVER) != 0u;
         const uint32_t lva = by_remote ? msg_u32(m, kMRemoteVa) : msg_u32(m, kMLocalVa);  // low 32 bits suffice
         uint32_t first = pmtu - lva % pmtu;
         first = total < first ? total : first;
@@ -305,6 +355,7 @@ __device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const
             g.plen = rem < pmtu ? rem : pmtu;
         }
     }
+    send_opcode(m, s, g);
     const uint32_t pad = (4u - (g.plen & 3u)) & 3u;
     g.L = 4u * g.hw + g.plen + pad + 4u;
     // UDP payload only (generate_payload_from_msg returns BTH .. ICRC, net/util.rs:183-185): the
@@ -324,23 +375,12 @@ __device__ __forceinline__ void plan_packet(const MsgRegs &m, uint32_t pk, const
 
 // Header words (LE u32 of header bytes 4w .. 4w+3): IPv4 (write_ip_udp_header,
 // packet_processor.rs:307-332) + UDP + BTH (set_from_common_meta, packet.rs:145-153, on a zeroed
-// buffer) + RETH (197-201) [+ secondary RETH, read requests].  Returned as lane w of one VGPR.
+// buffer) + RETH (197-201) [+ ImmDt | secondary RETH].  Returned as lane w of one VGPR.
 __device__ __forceinline__ uint32_t header_lanes(const MsgRegs &m, const SendPlan &g, uint32_t lane) {
     const uint32_t s = g.pk - msg_u32(m, kMFirst);
-    const uint32_t n = msg_u32(m, kMNpk), kind = msg_kind(m), tran = (msg_u32(m, kMKind) >> 8) & 0xffu;
+    const uint32_t kind = msg_kind(m), tran = (msg_u32(m, kMKind) >> 8) & 0xffu;
     const uint32_t flags = msg_flags(m);
-    const bool only = n == 1u, last = s + 1u == n;
-    uint32_t op, ack;
-    if (kind == 0u) {  // Write::handle (write.rs:31-96)
-        op = only ? 0x0Au : (s == 0u ? 0x06u : (last ? 0x08u : 0x07u));
-        ack = (only || last) ? 1u : 0u;
-    } else if (kind == 1u) {  // ReadResponse::handle (read_response.rs:30-95)
-        op = only ? 0x10u : (s == 0u ? 0x0Du : (last ? 0x0Fu : 0x0Eu));
-        ack = (only || last) ? 1u : 0u;
-    } else {  // Read::handle: ack_req = the request is signaled (read.rs:37)
-        op = 0x0Cu;
-        ack = (flags & ICRC_WRITE_ACK_REQ) ? 1u : 0u;
-    }
+    const uint32_t op = g.op, ack = g.ack;
     const uint32_t sol = (flags & ICRC_WRITE_SOLICITED) ? 0x80u : 0u;
     const uint32_t pad = (4u - (g.plen & 3u)) & 3u;
     const uint32_t msn_id = msg_u32(m, kMMsnId), msn = msn_id & 0xffffu, ipid = msn_id >> 16;
@@ -360,9 +400,10 @@ __device__ __forceinline__ uint32_t header_lanes(const MsgRegs &m, const SendPla
     w[10] = bswap32(static_cast<uint32_t>(va >> 32));
     w[11] = bswap32(static_cast<uint32_t>(va));
     w[12] = bswap32(msg_u32(m, kMRkey));
-    w[13] = bswap32(msg_u32(m, kMRethLen));
-    // secondary RETH of a read request: the local SGE (va, lkey, len)
-    w[14] = bswap32(msg_u32(m, kMLocalVa + 1));
+    w[13] = bswap32(g.rlen);
+    // secondary RETH of a read request: the local SGE (va, lkey, len); or the ImmDt (Immediate::set,
+    // big-endian, packet.rs:251-253) of a WRITE_*_WITH_IMMEDIATE packet
+    w[14] = bswap32(kind == 2u ? msg_u32(m, kMLocalVa + 1) : msg_u32(m, kMImm));
     w[15] = bswap32(msg_u32(m, kMLocalVa));
     w[16] = bswap32(msg_u32(m, kMLkey));
     w[17] = bswap32(msg_u32(m, kMTotal));

@@ -100,10 +100,14 @@ WRITE_MSG_DTYPE = np.dtype([
     ("psn", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("first_packet", "<u4"),
     ("npackets", "<u4"), ("slot_stride", "<u4"), ("msn", "<u2"), ("ip_id", "<u2"),
     ("kind", "u1"), ("tran_type", "u1"), ("flags", "u1"), ("_pad", "u1"), ("lkey", "<u4"),
+    ("imm", "<u4"), ("_rsvd", "<u4"),
 ])
-WRITE_FILL_IPV4_CSUM, WRITE_SEG_BY_REMOTE_VA, WRITE_SOLICITED, WRITE_ACK_REQ = 0x01, 0x02, 0x04, 0x08
+WRITE_FILL_IPV4_CSUM, WRITE_RUST_DRIVER, WRITE_SOLICITED, WRITE_ACK_REQ = 0x01, 0x02, 0x04, 0x08
+WRITE_SEG_BY_REMOTE_VA = WRITE_RUST_DRIVER  # BlueRDMALogic::send (logic.rs:168-271), see include/icrc.h
 WRITE_UDP_PAYLOAD_ONLY = 0x10  # BTH .. ICRC at each slot (generate_payload_from_msg's form)
-assert WRITE_MSG_DTYPE.itemsize == 88
+# ToCardWriteDescriptor is_first = false / is_last = false / WriteWithImm (types.rs:548-555, 641-648)
+WRITE_NOT_FIRST, WRITE_NOT_LAST, WRITE_WITH_IMM = 0x20, 0x40, 0x80
+assert WRITE_MSG_DTYPE.itemsize == 96
 MSG_WRITE, MSG_READ_RESPONSE, MSG_READ_REQUEST = 0, 1, 2
 
 # icrc_rx_desc (include/icrc.h): one parsed received packet.
@@ -483,7 +487,7 @@ def write_messages(specs, slot_stride: int = 0, base_out: int = 0) -> np.ndarray
         if int(s.get("kind", 0)) == MSG_READ_REQUEST:
             n = 1  # Read::handle sends one request packet (read.rs:33-89)
         else:
-            seg_va = s.get("remote_va", 0) if int(s.get("flags", 0)) & WRITE_SEG_BY_REMOTE_VA else s.get("local_va", 0)
+            seg_va = s.get("remote_va", 0) if int(s.get("flags", 0)) & WRITE_RUST_DRIVER else s.get("local_va", 0)
             n = write_segment_count(int(seg_va), int(s["total_len"]), int(s["pmtu"]))
         stride = int(s.get("slot_stride", slot_stride or max(128, (int(s.get("pmtu", 0)) + 64 + 3) & ~3)))
         m["npackets"], m["first_packet"], m["slot_stride"] = n, first, stride

@@ -286,6 +286,109 @@ uint32_t oracle_generate_segments(uint64_t va, uint32_t len, uint32_t path_mtu, 
     return n;
 }
 
+/* ---- rust_driver's send rule: BlueRDMALogic::send (rust_driver/src/device/software/logic.rs) ---- */
+
+/* ToHostWorkRbDescOpcode::is_first — rust_driver/src/device/types.rs:433-447 */
+static int opcode_is_first(uint8_t op) { return op == OP_WRITE_FIRST || op == OP_READ_RESP_FIRST; }
+
+/* get_first_packet_max_length — rust_driver/src/utils.rs:19-25 */
+static uint32_t first_packet_max_length(uint64_t va, uint32_t pmtu) { return pmtu - (uint32_t)(va % pmtu); }
+
+/* ToCardWriteDescriptor::write_only_opcode_with_imm — types.rs:558-581 */
+static uint8_t write_only_opcode_with_imm(const oracle_write_desc *d, int *with_imm) {
+    *with_imm = 0;
+    if (d->is_first && d->is_last) {
+        if (d->is_resp) return OP_READ_RESP_ONLY;
+        if (d->has_imm) { *with_imm = 1; return OP_WRITE_ONLY_IMM; }
+        return OP_WRITE_ONLY;
+    } else if (d->is_first) {
+        return d->is_resp ? OP_READ_RESP_FIRST : OP_WRITE_FIRST;
+    } else { /* "self.is_last = True" (also reached with is_last false) */
+        if (d->is_resp) return OP_READ_RESP_LAST;
+        if (d->has_imm) { *with_imm = 1; return OP_WRITE_LAST_IMM; }
+        return OP_WRITE_LAST;
+    }
+}
+
+/* write_first_opcode — types.rs:583-590 */
+static uint8_t write_first_opcode(const oracle_write_desc *d) {
+    if (d->is_first) return d->is_resp ? OP_READ_RESP_FIRST : OP_WRITE_FIRST;
+    return d->is_resp ? OP_READ_RESP_MIDDLE : OP_WRITE_MIDDLE;
+}
+
+/* write_middle_opcode — types.rs:592-598 */
+static uint8_t write_middle_opcode(const oracle_write_desc *d) {
+    return d->is_resp ? OP_READ_RESP_MIDDLE : OP_WRITE_MIDDLE;
+}
+
+/* write_last_opcode_with_imm — types.rs:600-609 */
+static uint8_t write_last_opcode_with_imm(const oracle_write_desc *d, int *with_imm) {
+    *with_imm = 0;
+    if (d->is_last) {
+        if (d->is_resp) return OP_READ_RESP_LAST;
+        if (d->has_imm) { *with_imm = 1; return OP_WRITE_LAST_IMM; }
+        return OP_WRITE_LAST;
+    }
+    return d->is_resp ? OP_READ_RESP_MIDDLE : OP_WRITE_MIDDLE;
+}
+
+static void logic_emit(oracle_logic_pkt *out, uint32_t max_out, uint32_t *n, uint8_t op, int with_imm,
+                       uint32_t imm, uint32_t psn, uint64_t va, uint32_t reth_len, uint32_t off, uint32_t len) {
+    if (*n < max_out) {
+        oracle_logic_pkt *p = &out[*n];
+        memset(p, 0, sizeof *p);
+        p->opcode = op;
+        p->has_imm = (uint8_t)(with_imm != 0);
+        p->imm = with_imm ? imm : 0u;
+        p->psn = psn & 0x00FFFFFFu;
+        p->reth_va = va;
+        p->reth_len = reth_len;
+        p->payload_off = off;
+        p->payload_len = len;
+    }
+    (*n)++;
+}
+
+/* BlueRDMALogic::send for ToCardDescriptor::Write — logic.rs:191-271, with
+ * send_write_only_packet (109-134).  Psn::wrapping_add is mod 2^24 (rust_driver/src/types.rs:180-183). */
+uint32_t oracle_logic_send(const oracle_write_desc *d, oracle_logic_pkt *out, uint32_t max_out) {
+    uint32_t n = 0;
+    if (d == NULL || d->pmtu == 0) return 0;
+    const uint32_t pmtu = d->pmtu;                                               /* 193 */
+    const uint32_t first_max = first_packet_max_length(d->raddr, pmtu);           /* 194 */
+    const uint32_t sge_total = d->sge_len;                                        /* 207 */
+    int with_imm = 0;
+    if (sge_total <= first_max) {                                                 /* 208-210 */
+        /* send_write_only_packet, 109-134 */
+        uint8_t op = write_only_opcode_with_imm(d, &with_imm);                    /* 118 */
+        uint32_t reth_len = opcode_is_first(op) ? d->total_len : sge_total;       /* 121-125 */
+        logic_emit(out, max_out, &n, op, with_imm, d->imm, d->psn, d->raddr, reth_len, 0, sge_total);
+        return n;
+    }
+    uint64_t cur_va = d->raddr;                                                   /* 214 */
+    uint32_t cur_len = sge_total;                                                 /* 215 */
+    uint32_t psn = d->psn;                                                        /* 216 */
+    uint32_t pos = 0;
+    const uint32_t first_len = first_max;                                         /* 220 */
+    uint8_t op = write_first_opcode(d);                                           /* 223 */
+    uint32_t reth_len = opcode_is_first(op) ? d->total_len : first_len;           /* 224-228 */
+    logic_emit(out, max_out, &n, op, 0, 0, psn, cur_va, reth_len, pos, first_len); /* 229-237 */
+    cur_len -= first_len;
+    psn = (psn + 1u) & 0x00FFFFFFu;
+    cur_va += first_len;
+    pos += first_len;
+    while (cur_len > pmtu) {                                                      /* 240-254 */
+        logic_emit(out, max_out, &n, write_middle_opcode(d), 0, 0, psn, cur_va, pmtu, pos, pmtu);
+        cur_len -= pmtu;
+        psn = (psn + 1u) & 0x00FFFFFFu;
+        cur_va += pmtu;
+        pos += pmtu;
+    }
+    op = write_last_opcode_with_imm(d, &with_imm);                                /* 256-270 */
+    logic_emit(out, max_out, &n, op, with_imm, d->imm, psn, cur_va, cur_len, pos, cur_len);
+    return n;
+}
+
 /* calculate_ipv4_checksum — rust_driver/src/responser.rs:321-338 */
 uint16_t oracle_ipv4_checksum(const uint8_t *h) {
     uint32_t sum = 0;

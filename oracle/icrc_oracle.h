@@ -103,6 +103,28 @@ int oracle_generate_ack(uint16_t pkey, uint32_t peer_qpn, uint32_t expected_psn,
 uint32_t oracle_generate_segments(uint64_t va, uint32_t len, uint32_t path_mtu, uint64_t *seg_va,
                                   uint32_t *seg_len, uint32_t max_segs);
 
+/* rust_driver's send rule, BlueRDMALogic::send (rust_driver/src/device/software/logic.rs:109-134,
+ * 168-271) for a WRITE / WRITE_WITH_IMM / READ_RESP descriptor (ToCardWriteDescriptor,
+ * types.rs:548-617).  One entry per RdmaMessage handed to NetSendAgent::send, in order; the payload
+ * is bytes [payload_off, payload_off + payload_len) of the descriptor's SG list (SGList::cut). */
+typedef struct oracle_write_desc {
+    uint64_t raddr;     /* common.raddr */
+    uint32_t total_len; /* common.total_len */
+    uint32_t sge_len;   /* sg_list.get_total_length() */
+    uint32_t pmtu;      /* u32::from(&common.pmtu) */
+    uint32_t psn;       /* common.psn */
+    uint32_t imm;       /* WriteWithImm's imm */
+    uint8_t is_resp;    /* ToCardWorkRbDescOpcode::ReadResp */
+    uint8_t is_first, is_last, has_imm;
+} oracle_write_desc;
+typedef struct oracle_logic_pkt {
+    uint64_t reth_va;
+    uint32_t psn, reth_len, imm, payload_off, payload_len;
+    uint8_t opcode, has_imm, _pad[2];
+} oracle_logic_pkt;
+/* Returns the number of messages (fills at most max_out). */
+uint32_t oracle_logic_send(const oracle_write_desc *d, oracle_logic_pkt *out, uint32_t max_out);
+
 /* responser.rs:321-338 (IPv4 header checksum, §8f row 4). */
 uint16_t oracle_ipv4_checksum(const uint8_t *hdr20);
 

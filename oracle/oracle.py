@@ -38,6 +38,27 @@ OP_READ_RESP_ONLY = 0x10
 OP_ACK = 0x11
 
 
+class WriteDesc(ctypes.Structure):
+    """oracle_write_desc (icrc_oracle.h): the ToCardWriteDescriptor fields BlueRDMALogic::send reads."""
+
+    _fields_ = [
+        ("raddr", ctypes.c_uint64), ("total_len", ctypes.c_uint32), ("sge_len", ctypes.c_uint32),
+        ("pmtu", ctypes.c_uint32), ("psn", ctypes.c_uint32), ("imm", ctypes.c_uint32),
+        ("is_resp", ctypes.c_uint8), ("is_first", ctypes.c_uint8), ("is_last", ctypes.c_uint8),
+        ("has_imm", ctypes.c_uint8),
+    ]
+
+
+class LogicPkt(ctypes.Structure):
+    """oracle_logic_pkt (icrc_oracle.h): one RdmaMessage BlueRDMALogic::send emits."""
+
+    _fields_ = [
+        ("reth_va", ctypes.c_uint64), ("psn", ctypes.c_uint32), ("reth_len", ctypes.c_uint32),
+        ("imm", ctypes.c_uint32), ("payload_off", ctypes.c_uint32), ("payload_len", ctypes.c_uint32),
+        ("opcode", ctypes.c_uint8), ("has_imm", ctypes.c_uint8), ("_pad", ctypes.c_uint8 * 2),
+    ]
+
+
 class RdmaMsg(ctypes.Structure):
     """Flattened RdmaMessage (types.rs); layout == oracle_rdma_msg in icrc_oracle.h."""
 
@@ -108,6 +129,8 @@ def lib() -> ctypes.CDLL:
             ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u8p, u8p, ctypes.c_uint32,
         ]
         L.oracle_generate_segments.restype = ctypes.c_uint32
+        L.oracle_logic_send.argtypes = [ctypes.POINTER(WriteDesc), ctypes.POINTER(LogicPkt), ctypes.c_uint32]
+        L.oracle_logic_send.restype = ctypes.c_uint32
         L.oracle_ipv4_checksum.argtypes = [u8p]
         L.oracle_ipv4_checksum.restype = ctypes.c_uint16
         L.oracle_mix64.argtypes = [ctypes.c_uint64]
@@ -227,6 +250,22 @@ def generate_segments(va: int, length: int, pmtu: int):
     return [(int(a), int(b)) for a, b in zip(sva, sl)]
 
 
+def logic_send(*, raddr: int, total_len: int, sge_len: int, pmtu: int, psn: int, is_resp: bool = False,
+               is_first: bool = True, is_last: bool = True, imm=None) -> list:
+    """BlueRDMALogic::send (rust_driver/src/device/software/logic.rs:191-271) for one WRITE /
+    WRITE_WITH_IMM / READ_RESP descriptor: the RdmaMessages it hands to NetSendAgent::send, as
+    dicts (opcode, psn, reth_va, reth_len, imm or None, payload_off, payload_len)."""
+    d = WriteDesc(raddr=raddr & 0xFFFFFFFFFFFFFFFF, total_len=total_len, sge_len=sge_len, pmtu=pmtu, psn=psn,
+                  imm=0 if imm is None else imm, is_resp=int(is_resp), is_first=int(is_first),
+                  is_last=int(is_last), has_imm=int(imm is not None))
+    n = lib().oracle_logic_send(ctypes.byref(d), None, 0)
+    out = (LogicPkt * max(n, 1))()
+    lib().oracle_logic_send(ctypes.byref(d), out, n)
+    return [dict(opcode=p.opcode, psn=p.psn, reth_va=p.reth_va, reth_len=p.reth_len,
+                 imm=p.imm if p.has_imm else None, payload_off=p.payload_off, payload_len=p.payload_len)
+            for p in out[:n]]
+
+
 def ipv4_checksum(hdr) -> int:
     a = _as_u8(hdr)
     return lib().oracle_ipv4_checksum(_ptr(a))
@@ -327,20 +366,33 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
             k = int(m["first_packet"])
             lens[k], icrcs[k] = pkt.size, int(pkt[-4:].view("<u4")[0])
             continue
-        seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])  # rust_driver utils.rs:19-33
-        segs = generate_segments(seg_va, int(m["total_len"]), int(m["pmtu"]))
-        assert len(segs) == int(m["npackets"])
-        only, first, middle, last = _SEND_OPCODES[int(m["kind"])]
+        if flags & 0x02:  # ICRC_WRITE_RUST_DRIVER: BlueRDMALogic::send (logic.rs:168-271)
+            plan = logic_send(raddr=int(m["remote_va"]), total_len=int(m["reth_len"]), sge_len=int(m["total_len"]),
+                              pmtu=int(m["pmtu"]), psn=int(m["psn"]), is_resp=int(m["kind"]) == 1,
+                              is_first=not flags & 0x20, is_last=not flags & 0x40,
+                              imm=int(m["imm"]) if (flags & 0x80 and int(m["kind"]) == 0) else None)
+            ack_all = 1 if flags & 0x08 else 0  # ack_req: false (logic.rs:184) unless ICRC_WRITE_ACK_REQ
+            plan = [(p["opcode"], ack_all, p["psn"], p["reth_va"], p["reth_len"], p["imm"], p["payload_len"])
+                    for p in plan]
+        else:
+            segs = generate_segments(int(m["local_va"]), int(m["total_len"]), int(m["pmtu"]))
+            only, first, middle, last = _SEND_OPCODES[int(m["kind"])]
+            plan, pos = [], 0
+            for s, (_, sl) in enumerate(segs):
+                if len(segs) == 1:
+                    op, ack = only, 1
+                elif s == 0:
+                    op, ack = first, 0
+                elif s + 1 == len(segs):
+                    op, ack = last, 1
+                else:
+                    op, ack = middle, 0
+                plan.append((op, ack, (int(m["psn"]) + s) & 0xFFFFFF,
+                             (int(m["remote_va"]) + pos) & 0xFFFFFFFFFFFFFFFF, int(m["reth_len"]), None, sl))
+                pos += sl
+        assert len(plan) == int(m["npackets"])
         pos = 0
-        for s, (_, sl) in enumerate(segs):
-            if len(segs) == 1:
-                op, ack = only, 1
-            elif s == 0:
-                op, ack = first, 0
-            elif s + 1 == len(segs):
-                op, ack = last, 1
-            else:
-                op, ack = middle, 0
+        for s, (op, ack, psn, reth_va, reth_len, imm, sl) in enumerate(plan):
             po = int(m["payload_offset"]) + pos
             payload = np.ascontiguousarray(src[po: po + sl])
             msg = RdmaMsg()
@@ -351,10 +403,12 @@ def send_messages(src: np.ndarray, msgs: np.ndarray, wire_bytes: int):
             msg.ack_req = ack
             msg.pkey = int(m["msn"])
             msg.dqpn = int(m["dqpn"])
-            msg.psn = (int(m["psn"]) + s) & 0xFFFFFFFF
-            msg.reth_va = (int(m["remote_va"]) + pos) & 0xFFFFFFFFFFFFFFFF
+            msg.psn = psn
+            msg.reth_va = reth_va
             msg.reth_rkey = int(m["rkey"])
-            msg.reth_len = int(m["reth_len"])
+            msg.reth_len = reth_len
+            msg.has_imm = 0 if imm is None else 1
+            msg.imm = 0 if imm is None else imm
             msg.payload = payload.ctypes.data if sl else None
             msg.payload_len = sl
             rc, pkt = packet_write(msg, int(m["src_ip"]), 4791, int(m["dst_ip"]), 4791, int(m["ip_id"]),

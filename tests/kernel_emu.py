@@ -68,13 +68,13 @@ def _bswap16(x: int) -> int:
 
 def packetizer_header_words(m, s: int) -> tuple:
     """icrc_packetize_kernel's plan_packet + header_lanes for packet s of message m (a
-    WRITE_MSG_DTYPE record): returns (14 or 18 LE header words, payload len, wire length L)."""
+    WRITE_MSG_DTYPE record): returns (14, 15 or 18 LE header words, payload len, wire length L)."""
     kind, flags = int(m["kind"]), int(m["flags"])
     if kind == 2:  # READ REQUEST: one packet, no payload, a secondary RETH (read.rs:57-74)
         start, ln, hw = 0, 0, 18
     else:
         total, pmtu = int(m["total_len"]), int(m["pmtu"])
-        seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])
+        seg_va = int(m["remote_va"]) if flags & 0x02 else int(m["local_va"])  # ICRC_WRITE_RUST_DRIVER
         first = min(total, pmtu - (seg_va & 0xFFFFFFFF) % pmtu)
         if s == 0:
             start, ln = 0, first
@@ -86,14 +86,31 @@ def packetizer_header_words(m, s: int) -> tuple:
     L = 4 * hw + ln + pad + 4
     n = int(m["npackets"])
     only, last = n == 1, s + 1 == n
-    if kind == 0:
-        op = 0x0A if only else (0x06 if s == 0 else (0x08 if last else 0x07))
-        ack = 1 if (only or last) else 0
-    elif kind == 1:
-        op = 0x10 if only else (0x0D if s == 0 else (0x0F if last else 0x0E))
-        ack = 1 if (only or last) else 0
-    else:
+    rlen = int(m["reth_len"])
+    if kind == 2:
         op, ack = 0x0C, 1 if flags & 0x08 else 0
+    elif not flags & 0x02:  # emulator: Write::handle / ReadResponse::handle
+        ONLY, FIRST, MIDDLE, LAST = (0x0A, 0x06, 0x07, 0x08) if kind == 0 else (0x10, 0x0D, 0x0E, 0x0F)
+        op = ONLY if only else (FIRST if s == 0 else (LAST if last else MIDDLE))
+        ack = 1 if (only or last) else 0
+    else:  # send_opcode, ICRC_WRITE_RUST_DRIVER
+        df, dl = not flags & 0x20, not flags & 0x40
+        imm = kind == 0 and bool(flags & 0x80)
+        ONLY, FIRST, MIDDLE = (0x0A, 0x06, 0x07) if kind == 0 else (0x10, 0x0D, 0x0E)
+        LAST = 0x0F if kind == 1 else (0x09 if imm else 0x08)
+        if only:
+            op = (0x0B if imm else ONLY) if (df and dl) else (FIRST if df else LAST)
+        elif s == 0:
+            op = FIRST if df else MIDDLE
+        elif not last:
+            op = MIDDLE
+        else:
+            op = LAST if dl else MIDDLE
+        ack = 1 if flags & 0x08 else 0
+        rlen = rlen if op == FIRST else ln
+        if op in (0x09, 0x0B):
+            hw = 15
+            L = 4 * hw + ln + pad + 4
     sol = 0x80 if flags & 0x04 else 0
     psn = (int(m["psn"]) + s) & 0xFFFFFF
     va = (int(m["remote_va"]) + start) & 0xFFFFFFFFFFFFFFFF
@@ -111,7 +128,9 @@ def packetizer_header_words(m, s: int) -> tuple:
     w[10] = _bswap32(va >> 32)
     w[11] = _bswap32(va & 0xFFFFFFFF)
     w[12] = _bswap32(int(m["rkey"]))
-    w[13] = _bswap32(int(m["reth_len"]))
+    w[13] = _bswap32(rlen)
+    if hw == 15:
+        w[14] = _bswap32(int(m["imm"]))
     if hw == 18:
         lva = int(m["local_va"])
         w[14] = _bswap32(lva >> 32)

@@ -375,7 +375,7 @@ def test_rx_desc_layouts_agree():
     import icrc_amd
 
     assert icrc_amd.RX_DESC_DTYPE == oracle.RX_DESC_DTYPE
-    assert icrc_amd.WRITE_MSG_DTYPE.itemsize == 88
+    assert icrc_amd.WRITE_MSG_DTYPE.itemsize == 96
 
 
 def test_rx_parse_oracle_matches_kernel_model():

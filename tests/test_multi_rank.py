@@ -139,6 +139,32 @@ def test_bench_launcher_sums_failures_and_fails():
     assert res["parity_sample"]["failures_all_ranks"] == 1
 
 
+def test_bench_launcher_kills_stalled_ranks():
+    """A rank that never reaches the first barrier: the launcher's --launch-timeout kills the whole
+    rank group (torchrun + ranks, one session) and exits 3 with a one-line JSON error, well inside
+    the driver's own limit."""
+    import time
+
+    t0 = time.monotonic()
+    rc, res, err = _bench("--gpus", "2", "--packets", "8", "--stall-rank", "1", "--dist-timeout", "600",
+                          "--launch-timeout", "20")
+    assert rc == 3, err[-2000:]
+    assert res["value"] is None and "timed out" in res["error"]
+    assert time.monotonic() - t0 < 120
+
+
+def test_bench_collective_timeout_ends_ranks():
+    """The same stall with a short --dist-timeout: the waiting rank's barrier raises (gloo honours the
+    process-group timeout), torchrun tears the group down, and bench exits non-zero."""
+    import time
+
+    t0 = time.monotonic()
+    rc, res, err = _bench("--gpus", "2", "--packets", "8", "--stall-rank", "1", "--dist-timeout", "8",
+                          "--launch-timeout", "200")
+    assert rc not in (0, 3), err[-2000:]
+    assert time.monotonic() - t0 < 150
+
+
 def test_bench_refuses_world_size_mismatch():
     rc, res, _ = _bench("--gpus", "2", "--packets", "8", env_extra={"WORLD_SIZE": "1", "RANK": "0"})
     assert rc == 2 and res is None
