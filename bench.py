@@ -383,7 +383,21 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
     return fails, checked
 
 
-PMC_TRAFFIC_FILE = "r03_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r04_pmc_traffic.json"
+# the sources the C1 kernel is built from: a traffic summary taken on another build is not this one's
+KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp",
+                  "icrc_capi.cpp")
+
+
+def kernel_source_hash() -> str:
+    """sha256 (16 hex digits) over the C1 kernel's sources as shipped in this tree."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "open-rdma-driver_amd", "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 LOADS_ONLY_VARIANT = 19  # A/B library: icrc_batch_kernel<.., S = 2, D = 1, loads only>, the default ring without the CRC
 
 
@@ -392,7 +406,7 @@ def pmc_traffic(n: int, L: int):
     (FETCH_SIZE and WRITE_SIZE in separate runs of this same bench command, FETCH_SIZE corrected
     by the membench calibration; scripts/gpu_check.sh PMC=1 -> scripts/pmc_summary.py).  A bench
     process cannot read its own counters, so the committed summary is used when it was taken on
-    this exact workload; otherwise None."""
+    this exact workload AND this build of the kernel (kernel_source_hash); otherwise None."""
     path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
     try:
         with open(path) as f:
@@ -400,6 +414,10 @@ def pmc_traffic(n: int, L: int):
     except (OSError, ValueError):
         return None
     if tr.get("packets") != n or tr.get("packet_bytes") != L:
+        return None
+    if tr.get("source_hash") != kernel_source_hash():  # profiled on another build of the kernel
+        log(f"bench.py: profiles/{PMC_TRAFFIC_FILE} is of kernel sources {tr.get('source_hash')}, this tree is "
+            f"{kernel_source_hash()}: roofline.traffic left null")
         return None
     return tr
 

@@ -64,7 +64,11 @@ extern "C" {
 /* verify result byte values */
 #define ICRC_VERIFY_MISMATCH 0u
 #define ICRC_VERIFY_OK 1u
-#define ICRC_VERIFY_BADLEN 0xFFu /* device batches: len < 44 (counted in *d_nerr) */
+/* device batches: len < 44 (counted in *d_nerr).  Also the short-packet kernel's safety net: a wave
+ * whose frame bookkeeping would not terminate (never observed; it exists so that a bug ends in
+ * flagged results, not in a hung GPU) reports every packet of its range as BADLEN (compute: ICRC 0)
+ * and adds them to *d_nerr — pass d_nerr to see it. */
+#define ICRC_VERIFY_BADLEN 0xFFu
 
 typedef struct icrc_engine icrc_engine;
 
@@ -93,7 +97,7 @@ void *icrc_engine_stream(const icrc_engine *engine);
  *        compacting long-packet walker);
  *   301 / 302  the receive parse as one fused pass on any batch (S = 2 / S = 1).
  * Other values: ICRC_EINVAL.  The quad kernels (20, 24-26, 120-126, 220-226) and the diagnostics
- * whose results are wrong by design (15, 18, 19, 21, 22, 31, 32, 35, 41-48, 141-148, 241-248)
+ * whose results are wrong by design (15, 18, 19, 21, 22, 31, 32, 35, 41-53, 141-153, 241-253)
  * exist only in the A/B library libicrc_amd_ab.so (built with ICRC_AB_BUILD), which no product
  * path loads. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);

@@ -170,6 +170,9 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     }
     p.variant = short_variant;
     p.split_len = split;
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_SPLIT = the length split of ragged batches (oct takes L < split)
+    if (const char *v = std::getenv("ICRC_AB_SPLIT")) p.split_len = std::min<uint32_t>(split, static_cast<uint32_t>(std::atoi(v)));
+#endif
     // Default: both halves in one launch (the fused hybrid kernel).  A forced hybrid variant
     // (100 + q, 200 + q: A/B) keeps the two-stream fork / join below.
     if (!hybrid_forced) {
@@ -1060,6 +1063,10 @@ int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t s
     p.pkt_len = d_pkt_len;
     p.icrc = d_icrc;
     p.table = e->d_table;
+    p.rotate = 1;
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK_ROT=0 walks every wave's chunk in order
+    if (const char *v = std::getenv("ICRC_AB_PK_ROT")) p.rotate = static_cast<uint32_t>(std::atoi(v));
+#endif
     return icrc::launch_packetize(p, grid_for(e, npackets), stream);
 }
 

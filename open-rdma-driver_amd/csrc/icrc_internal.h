@@ -151,6 +151,7 @@ struct PacketizeParams {
     uint32_t *pkt_len;
     uint32_t *icrc;
     const uint32_t *table;
+    uint32_t rotate;  // 1: each wave starts its chunk at a hashed packet and wraps (default); 0: in order (A/B)
 };
 int launch_packetize(const PacketizeParams &p, int grid, void *stream);
 int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, uint8_t *out, uint32_t stride,

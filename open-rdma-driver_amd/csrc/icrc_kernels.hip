@@ -42,10 +42,10 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_long_kernel(BatchParams
 
 // Kernel variants (runtime-selected, identical results):
 //   0            one packet per wave at a time, no pipelining, strided packet assignment
-//   S, D, ABL    pipelined with S chains and a D-deep ring over a contiguous packet chunk per
-//                wave; ABL = 0 (real), 1 (loads only, no CRC: a memory-pipeline bound),
-//                2 (CRC only, no loads: a compute bound); TRAILER: write / zero the trailers.
-template <int MODE, int S, int D, int ABL, bool TRAILER>
+//   S, D, A      pipelined with S chains and a D-deep ring over a contiguous packet chunk per
+//                wave; A = the ring's policy (Ring<aux, prio>, icrc_long.h; RingAblation in the A/B
+//                library); TRAILER: write / zero the trailers.
+template <int MODE, int S, int D, class A, bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     const char *lds = reinterpret_cast<const char *>(lds4);
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_batch_kernel(BatchParam
         if (!p.spread) wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew >> 16, lo64, hi64);
         const uint32_t lo = lo64 < p.n ? static_cast<uint32_t>(lo64) : p.n;
         const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo);
-        run_pipelined<MODE, S, D, ABL, 0, false, TRAILER, true>(p, lds, c, lane, lo, nq, &tv);
+        run_pipelined<MODE, S, D, A, 0, false, TRAILER, true>(p, lds, c, lane, lo, nq, &tv);
     }
 }
 
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_rx_kernel(BatchParams p
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = (p.n - lo) < chunk ? (p.n - lo) : chunk;
-    run_pipelined<kVerify, S, D, kStreamAux << 2, PARSE, false, TRAILER>(p, lds, c, lane, lo, nq);
+    run_pipelined<kVerify, S, D, Ring<kStreamAux>, PARSE, false, TRAILER>(p, lds, c, lane, lo, nq);
 }
 
 // ---- receive parse, pass 2 (icrc_rx_parse_device default) ----------------------------------
@@ -469,7 +469,8 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                                                                           const icrc_write_msg *msgs, uint32_t nmsgs,
                                                                           uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
                                                                           uint32_t *pkt_len,
-                                                                          uint32_t *icrc_out, const uint32_t *table) {
+                                                                          uint32_t *icrc_out, const uint32_t *table,
+                                                                          uint32_t rotate) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     table_fill(lds4, table);
     const char *lds = reinterpret_cast<const char *>(lds4);
@@ -486,19 +487,29 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t hi = (npk - lo) < chunk ? npk : lo + chunk;
 
-    // message holding packet lo: binary search on first_packet
-    int mlo = 0, mhi = static_cast<int>(nmsgs) - 1;
-    while (mlo < mhi) {
-        const int mid = (mlo + mhi + 1) >> 1;
-        if (msg_first_packet(msgs, mid) <= lo) mlo = mid;
-        else mhi = mid - 1;
-    }
-    mlo = __builtin_amdgcn_readfirstlane(mlo);
+    // The wave walks its chunk starting at a hashed packet and wrapping around, so that the 4096
+    // waves' read and write streams (chunks a fixed number of bytes apart) do not advance through
+    // the memory channels in lockstep, whatever the buffers' physical placement.
+    const uint32_t n = hi - lo;
+    const uint32_t rot = rotate ? ((gw * 2654435761u) >> 7) % n : 0u;
 
-    // load side: one message cursor; the plan of packet pk (or an empty slot past hi)
+    // message holding packet pk: binary search on first_packet
+    auto find_msg = [&](uint32_t pk) __attribute__((always_inline)) -> int {
+        int a = 0, b = static_cast<int>(nmsgs) - 1;
+        while (a < b) {
+            const int mid = (a + b + 1) >> 1;
+            if (msg_first_packet(msgs, mid) <= pk) a = mid;
+            else b = mid - 1;
+        }
+        return __builtin_amdgcn_readfirstlane(a);
+    };
+    int mlo = find_msg(lo + rot);
+    const int mwrap = rot ? find_msg(lo) : mlo;
+
+    // load side: one message cursor; the plan of packet pk (or an empty slot past the chunk)
     MsgRegs lm;
     lm.idx = -1;
-    uint32_t next_pk = lo;
+    uint32_t next_t = 0;  // packets of the chunk issued so far; the next is lo + (next_t + rot) mod n
     bool slow_seen = false;
     auto locate = [&](MsgRegs &m, uint32_t pk, SendPlan &g) __attribute__((always_inline)) {
         while (m.idx < static_cast<int>(nmsgs) && (m.idx < 0 || pk >= msg_u32(m, kMFirst) + msg_u32(m, kMNpk)))
@@ -513,9 +524,14 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     // next packet of the ring (fast packets only), its header lanes and its row loads
     auto fill = [&](SendPlan &g, uint32_t &hvec, uint32_t (&u)[kRows]) __attribute__((always_inline)) {
         plan_empty(g);
-        while (next_pk < hi) {
-            locate(lm, next_pk, g);
-            ++next_pk;
+        while (next_t < n) {
+            const uint32_t t = next_t + rot;
+            if (t == n) {  // wrapped to the chunk's first packet: restart the message cursor there
+                lm.idx = -1;
+                mlo = mwrap;
+            }
+            locate(lm, lo + (t >= n ? t - n : t), g);
+            ++next_t;
             if (g.fast) break;
             slow_seen = true;
             plan_empty(g);
@@ -614,6 +630,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     if (slow_seen) {
         MsgRegs sm;
         sm.idx = -1;
+        mlo = mwrap;
         for (uint32_t pk = lo; pk < hi; ++pk) {
             SendPlan sg;
             locate(sm, pk, sg);
@@ -811,19 +828,27 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 // variant 16 without the raised wave priority around its load bursts; 20, 24-26, 31, 32, 35: the quad /
 // chunked oct kernels (icrc_quad.hip); 40: the fixed-frame oct kernel (icrc_oct.hip, default
 // for short packets).
+using RingNt = Ring<kStreamAux>;
+using RingNtNoPrio = Ring<kStreamAux, false>;
+#ifdef ICRC_AB_BUILD
+using RingLoadsOnly = RingAblation<kStreamAux, kCutLoadsOnly>;
+using RingCrcOnly = RingAblation<kStreamAux, kCutCrcOnly>;
+using RingNoFinal = RingAblation<kStreamAux, kCutNoFinal>;
+using RingNoStore = RingAblation<kStreamAux, kCutNoStore>;
+#endif
 template <int MODE>
 static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     switch (p.variant) {
-    case 0: ICRC_LAUNCH_T(0, 1, 0); break;
-    case 13: ICRC_LAUNCH_T(1, 1, 2 << 2); break;              // S = 1, nt row loads
-    case 17: ICRC_LAUNCH_T(2, 1, (2 << 2) | kAblNoPrio); break;  // 16 without the raised priority (A/B)
+    case 0: ICRC_LAUNCH_T(0, 1, Ring<0>); break;
+    case 13: ICRC_LAUNCH_T(1, 1, RingNt); break;        // S = 1, nt row loads
+    case 17: ICRC_LAUNCH_T(2, 1, RingNtNoPrio); break;  // 16 without the raised priority (A/B)
     case 40: (void)launch_oct(MODE, p, grid, s); break;
 #ifdef ICRC_AB_BUILD  // the A/B library only: quad kernels and diagnostics (wrong results by design)
-    case 15: ICRC_LAUNCH(1, 2, 1 | (2 << 2), false); break;  // diagnostic: loads only, nt
-    case 18: ICRC_LAUNCH(1, 2, 2 | (2 << 2), false); break;  // diagnostic: CRC only (same shape as 15)
-    case 19: ICRC_LAUNCH(2, 1, 1 | (2 << 2), false); break;  // diagnostic: loads only of the default (16) ring
-    case 21: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoFinal, false); break;  // diagnostic: 16 without final products
-    case 22: ICRC_LAUNCH(2, 1, (2 << 2) | kAblNoStore, false); break;  // diagnostic: 16 without result stores
+    case 15: ICRC_LAUNCH(1, 2, RingLoadsOnly, false); break;  // loads only, nt
+    case 18: ICRC_LAUNCH(1, 2, RingCrcOnly, false); break;   // CRC only (as 15)
+    case 19: ICRC_LAUNCH(2, 1, RingLoadsOnly, false); break;  // loads only of 16's ring
+    case 21: ICRC_LAUNCH(2, 1, RingNoFinal, false); break;   // 16 without final products
+    case 22: ICRC_LAUNCH(2, 1, RingNoStore, false); break;   // 16 without result stores
     case 20:
     case 24:
     case 25:
@@ -845,7 +870,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 52: (void)launch_oct(MODE, p, grid, s, 12); break;  // diagnostic: block preparation reused (strided)
     case 53: (void)launch_oct(MODE, p, grid, s, 13); break;  // diagnostic: per-wave start / end stamps
 #endif
-    default: ICRC_LAUNCH_T(2, 1, 2 << 2); break;  // 16: S = 2, nt row loads
+    default: ICRC_LAUNCH_T(2, 1, RingNt); break;  // 16: S = 2, nt row loads
     }
 }
 #undef ICRC_LAUNCH_T
@@ -939,7 +964,7 @@ int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((icrc_packetize_kernel<1>), dim3(grid), dim3(kThreadsPerGroup), 0,
                        static_cast<hipStream_t>(stream), p.src, p.src_bytes, p.msgs, p.nmsgs, p.npackets, p.wire,
-                       p.wire_bytes, p.pkt_len, p.icrc, p.table);
+                       p.wire_bytes, p.pkt_len, p.icrc, p.table, p.rotate);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -91,17 +91,32 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
 
 // Loads of one packet's rows; rows past the
 // packet and every row of a non-regular slot read 0 through the descriptor's range check.
-// ABL = mode | (cache policy << 2): mode 0 real, 1 loads only, 2 CRC only; policy = the aux
-// operand of the row loads (0 default, 2 nt: read-once stream).
-// kAblNoPrio: leave the wave priority alone around the load burst (A/B: variant 17).
-constexpr int kAblNoPrio = 1 << 8;
-// kAblNoFinal (diagnostic, variant 21): skip the per-lane final product M^(64-l) (wrong results)
-constexpr int kAblNoFinal = 1 << 9;
-// kAblNoStore (diagnostic, variant 22): the result stores of every block but the chunk's last
-constexpr int kAblNoStore = 1 << 10;
-constexpr int abl_mode(int abl) { return abl & 3; }
-constexpr int abl_aux(int abl) { return (abl >> 2) & 0x3F; }
-constexpr bool abl_prio(int abl) { return (abl & kAblNoPrio) == 0; }
+// The ring's policy: the cache policy of its row loads (the aux operand: 0 default, 2 nt, a
+// read-once stream) and whether the wave raises its priority around a load burst.  The product
+// runs Ring<kStreamAux> (and Ring<kStreamAux, false>, A/B variant 17).  The A/B library also
+// instantiates RingAblation<...> (ICRC_AB_BUILD), which switch a part off so that its cost can be
+// measured on the same build (results wrong by design).
+template <int AUX, bool PRIO = true>
+struct Ring {
+    static constexpr int kAux = AUX;
+    static constexpr bool kPrio = PRIO;
+    static constexpr bool kLoads = true;   // the row loads (else synthetic rows: a compute bound)
+    static constexpr bool kSteps = true;   // the row steps (else the rows XOR-folded: a memory-pipeline bound)
+    static constexpr bool kFinal = true;   // the per-lane final products M^(64 - l)
+    static constexpr bool kStores = true;  // the result stores of every block
+};
+#ifdef ICRC_AB_BUILD
+// LOADS_ONLY: variants 15, 19 (the loads-only denominator bench.py reports); CRC_ONLY: 18;
+// NO_FINAL: 21; NO_STORE: 22 (the result stores of every block but the chunk's last).
+enum RingCut { kCutLoadsOnly, kCutCrcOnly, kCutNoFinal, kCutNoStore };
+template <int AUX, int CUT>
+struct RingAblation : Ring<AUX> {
+    static constexpr bool kLoads = CUT != kCutCrcOnly;
+    static constexpr bool kSteps = CUT != kCutLoadsOnly;
+    static constexpr bool kFinal = CUT != kCutNoFinal;
+    static constexpr bool kStores = CUT != kCutNoStore;
+};
+#endif
 
 // Verify runs over the trailer as the stream's last word (kIcrcResidue, icrc_device.h): the same
 // kRows loads per slot as compute.
@@ -111,15 +126,16 @@ constexpr int ring_words() { return kRows; }
 // TRAILER: the row holding the trailer's line (the last) and the verify trailer word load with the
 // default policy, so the line is in L2 when the trailer store / zeroing follows
 // (scripts/trailerbench.hip T9: 0.8615 vs 0.877 ms with every row nt).
-template <int ABL, int MODE, bool TRAILER = false>
+template <class A, int MODE, bool TRAILER = false>
 __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint32_t (&u)[ring_words<MODE>()]) {
-    if constexpr (abl_mode(ABL) == 2) {
+    if constexpr (!A::kLoads) {
 #pragma unroll
         for (int j = 0; j < ring_words<MODE>(); ++j) u[j] = lane * 0x9E3779B9u + static_cast<uint32_t>(j) * 0x85EBCA6Bu;
         return;
     }
-    constexpr int kAux = abl_aux(ABL);
-    // compute reads [0, L-4); verify also the trailer [L-4, L) (rows never reach it)
+    constexpr int kAux = A::kAux;
+    // compute reads [0, L-4); verify also the trailer [L-4, L): it is the last word of the loaded
+    // rows (verify by residue, kIcrcResidue)
     const int nrec = m.kind == 1 ? static_cast<int>(MODE == kVerify ? m.L : m.L - 4u) : 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, nrec, 0x00020000);
     const uint32_t vbase = 4u * static_cast<uint32_t>(m.k0 - 1 + static_cast<int>(lane));
@@ -139,14 +155,13 @@ __device__ __forceinline__ void slot_load(const SlotMeta &m, uint32_t lane, uint
 // verify: zeros, is_icrc_valid, 350) as a buffer store that every lane issues, lane 0 in range
 // (no branch, so the ring's vmcnt accounting stays exact; an empty slot's descriptor has size 0).
 template <int MODE, bool TRAILER>
-__device__ __forceinline__ uint32_t regular_result(const SlotMeta &m, uint32_t crc, uint32_t stored, uint32_t lane) {
+__device__ __forceinline__ uint32_t regular_result(const SlotMeta &m, uint32_t crc, uint32_t lane) {
     if constexpr (TRAILER) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(m.pkt, 0, m.kind == 1 ? static_cast<int>(m.L) : 0, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, rs,
                                               static_cast<int>(lane == 0 ? m.L - 4u : 0x80000000u), 0, 0);
     }
-    (void)stored;
     if constexpr (MODE == kCompute) return crc;
     else return crc == kIcrcResidue ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;
 }
@@ -423,7 +438,7 @@ __device__ __forceinline__ void rx_acc_flush(const BatchParams &p, RxAcc &a, uin
 // the wave's result buffer.
 // PARSE: 0 off; 1 receive parse, a descriptor store per packet (rx_store; A/B variant 301);
 // 2 receive parse into RxAcc (the fused receive of small batches).
-template <int MODE, int S, int ABL, int PARSE = 0, bool TRAILER = false>
+template <int MODE, int S, class A, int PARSE = 0, bool TRAILER = false>
 __device__ __forceinline__ void process_set(const BatchParams &p, const char *lds, const LaneConsts &c,
                                             uint32_t lane, const SlotMeta (&m)[S],
                                             uint32_t (&u)[S][ring_words<MODE>()], uint32_t q0, ResultBuf &rb,
@@ -464,7 +479,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
             for (int j = 1; j < kRows; ++j) {
 #pragma unroll
                 for (int s = 0; s < S; ++s) {
-                    if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                    if constexpr (!A::kSteps) acc[s] ^= u[s][j];
                     else acc[s] = step_m64(lds, acc[s], u[s][j], c);
                 }
             }
@@ -474,7 +489,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                 if (j < rmax) {
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        if constexpr (abl_mode(ABL) == 1) acc[s] ^= u[s][j];
+                        if constexpr (!A::kSteps) acc[s] ^= u[s][j];
                         else acc[s] = step_m64(lds, acc[s], u[s][j], c);
                     }
                 }
@@ -486,7 +501,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
                 if (j < rmax) {
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        if constexpr (abl_mode(ABL) == 1) {
+                        if constexpr (!A::kSteps) {
                             acc[s] ^= u[s][j];
                         } else {
                             const uint32_t t = step_m64(lds, acc[s], u[s][j], c);
@@ -498,10 +513,10 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
         }
         uint32_t fin[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s) fin[s] = (ABL & kAblNoFinal) ? acc[s] : final_mul(lds, acc[s], c.fin);
+        for (int s = 0; s < S; ++s) fin[s] = A::kFinal ? final_mul(lds, acc[s], c.fin) : acc[s];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]), 0u, lane);
+            const uint32_t r = regular_result<MODE, TRAILER>(m[s], ~wave_xor(fin[s]), lane);
             if (m[s].kind == 1) {
                 rb_put(rb, q0 + s, r);
                 if constexpr (PARSE == 1)
@@ -532,7 +547,7 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // it waits for the table share, so that the three memory latencies overlap (a small batch, one
 // packet per wave, is made of little else); then every wave, with or without packets, writes its
 // share to LDS and joins the barrier.
-template <int MODE, int S, int D, int ABL, int PARSE = 0, bool LONG = false, bool TRAILER = false, bool TABLE = false>
+template <int MODE, int S, int D, class A, int PARSE = 0, bool LONG = false, bool TRAILER = false, bool TABLE = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq, TableShare *tv = nullptr) {
     constexpr int B = D + 1;
@@ -564,7 +579,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 slot_meta<MODE, LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
-                slot_load<ABL, MODE, TRAILER>(m[d][s], lane, u[d][s]);
+                slot_load<A, MODE, TRAILER>(m[d][s], lane, u[d][s]);
             }
         }
     }
@@ -582,21 +597,21 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             // unconditional: past the end slot_meta yields kind 0 (zero-size descriptor).  The burst
             // runs at raised wave priority, so the loads leave ahead of the other waves' row steps
             // (scripts/overlapbench.hip: the C1 walk 0.667 -> 0.648 ms against 0.638 loads-only).
-            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(3);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 slot_meta<MODE, LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
-                slot_load<ABL, MODE, TRAILER>(m[bp][s], lane, u[bp][s]);
+                slot_load<A, MODE, TRAILER>(m[bp][s], lane, u[bp][s]);
             }
-            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(0);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(0);
             const uint32_t q0 = ts * S;
-            process_set<MODE, S, ABL, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, ra, lo);
+            process_set<MODE, S, A, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, ra, lo);
             const uint32_t qn = q0 + S;  // next unprocessed
             if ((qn & 63u) == 0 || qn >= nq) {
                 if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
-                // kAblNoStore: only the chunk's last block is stored (its lanes depend on every
+                // !A::kStores (A/B): only the chunk's last block is stored (its lanes depend on every
                 // earlier packet through rb_put's selects, so nothing is dead code)
-                if constexpr ((ABL & kAblNoStore) == 0) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+                if constexpr (A::kStores) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
                 else if (qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
             }
             return true;
@@ -615,7 +630,7 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 // Packets in flight ahead of the one being stepped (3 measured the same on C2: the long half's
 // tail is the CUs freeing up from the short-packet kernel, not the walk's latency).
 constexpr int kLongWalkDepth = 1;
-template <int MODE, int D, int ABL, bool TRAILER>
+template <int MODE, int D, class A, bool TRAILER>
 __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
                                                    uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -679,7 +694,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         next(m[d][0], qs[d]);
-        slot_load<ABL, MODE, TRAILER>(m[d][0], lane, u[d][0]);
+        slot_load<A, MODE, TRAILER>(m[d][0], lane, u[d][0]);
         if (m[d][0].kind) inflight += 1;
     }
     for (;;) {
@@ -687,9 +702,9 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
             constexpr int b = decltype(bc)::value;
             constexpr int bp = (b + D) % B;
             next(m[bp][0], qs[bp]);
-            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(3);
-            slot_load<ABL, MODE, TRAILER>(m[bp][0], lane, u[bp][0]);
-            if constexpr (abl_prio(ABL)) __builtin_amdgcn_s_setprio(0);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(3);
+            slot_load<A, MODE, TRAILER>(m[bp][0], lane, u[bp][0]);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(0);
             if (m[bp][0].kind) inflight += 1;
             if (m[b][0].kind) {
                 const int blk = static_cast<int>(qs[b] >> 6);
@@ -697,7 +712,7 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
                     if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
                     rb_block = blk;
                 }
-                process_set<MODE, 1, ABL, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
+                process_set<MODE, 1, A, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
                 inflight -= 1;
             }
             return true;
@@ -762,7 +777,7 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
     if constexpr (COMPACT) {
-        run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+        run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER>(p, lds, c, lane, lo, nq);
     } else {
         // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
         // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
@@ -771,9 +786,9 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, kStreamAux << 2, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
+            run_pipelined<MODE, 2, 1, Ring<kStreamAux>, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
         else
-            run_pipelined_long<MODE, kLongWalkDepth, kStreamAux << 2, TRAILER>(p, lds, c, lane, lo, nq);
+            run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER>(p, lds, c, lane, lo, nq);
     }
 }
 

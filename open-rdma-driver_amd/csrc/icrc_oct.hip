@@ -247,10 +247,10 @@ __device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, ui
 }
 
 // One frame's rows, dispatched on its (uniform) flags.
-template <int MODE, bool TRAILER, int DIAG>
+template <int MODE, bool TRAILER, class D>
 __device__ __forceinline__ uint32_t oct_frame(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm, const char *lds,
                                               const LaneConsts &c) {
-    if constexpr (DIAG == 1 || DIAG == 3 || DIAG == 4 || DIAG == 5) {
+    if constexpr (!D::kRows) {
 #pragma unroll
         for (int j = 0; j < kOctK; ++j) acc ^= S.u[j];
         return acc;
@@ -301,30 +301,50 @@ __device__ __forceinline__ void oct_rows2(const OctSlot<MODE, TRAILER> &A, const
     accB = xb;
 }
 
-// DIAG (ablation builds, variants 41-48): 1 = the loads without the row steps and final
-// products, 2 = the row steps without the loads, 3 = neither loads nor row steps (control and
-// final products), 4 = control only, 5 = 1 without the per-frame stores, 6 = the full kernel
-// without the per-frame stores, 7 = the full kernel without the final products, 8 = the full
-// kernel with each set's per-lane packet data taken from the lane itself (no bperm before the
-// loads).
-// 9 / 10 = the full kernel / the loads-only build with each set's per-lane packet data computed
-// from the index (strided uniform batches only: no ds_bpermute on the path to a frame's loads;
-// wrong on anything else); 11 = the full kernel without the raised wave priority; 12 = the full
-// kernel with the per-block preparation (classification, sort, frame schedule) done once per wave
-// and reused (strided batches of uniform full blocks only); 13 = the full kernel, then each wave
-// stamps its start and end (s_memrealtime, 100 MHz) over its first four results (load balance).
-constexpr int oct_diag_base(int d) { return d == 10 ? 1 : (d == 9 || d == 11 || d == 12 || d == 13) ? 0 : d; }
-template <int MODE, bool RAGGED, bool TRAILER, int DIAGX>
+// The kernel's measurement policy.  The product instantiates OctProduct: every step real.  The
+// A/B library (ICRC_AB_BUILD) also instantiates OctAblation<X> (variants 41-53), each switching
+// one part off or replacing it, so that a part's cost can be measured on the same build
+// (results wrong by design except 48, 49, 51-53).
+struct OctProduct {
+    static constexpr bool kLoads = true;       // the row loads (else: synthetic rows, no memory)
+    static constexpr bool kRows = true;        // the row steps (else: the rows XOR-folded)
+    static constexpr bool kFinal = true;       // the final products M^(8 - c)
+    static constexpr bool kStores = true;      // result and trailer stores
+    static constexpr bool kSetPerm = true;     // a set's per-lane packet data from the sorted block entries
+    static constexpr bool kArithSetup = false; // ... or computed from the index (strided batches only)
+    static constexpr bool kPrio = true;        // raised wave priority over a frame's setup and loads
+    static constexpr bool kReusePrep = false;  // the first block's preparation reused (strided, full blocks)
+    static constexpr bool kStamp = false;      // each wave stamps start / end times over its first results
+};
+#ifdef ICRC_AB_BUILD
+// 41 loads only; 42 row steps, no loads; 43 control and final products; 44 control only; 45 = 41
+// without stores; 46 the full kernel without stores; 47 without final products; 48 each set's
+// packet data from the lane's own block entry; 49 / 50 the full kernel / loads only with the
+// packet data computed from the index; 51 without the raised priority; 52 the block preparation
+// reused; 53 with start / end stamps (scripts/probe_oct_balance.py).
+template <int X>
+struct OctAblation : OctProduct {
+    static constexpr bool kLoads = !(X == 2 || X == 3 || X == 4);
+    static constexpr bool kRows = !(X == 1 || X == 3 || X == 4 || X == 5 || X == 10);
+    static constexpr bool kFinal = !(X == 1 || X == 4 || X == 5 || X == 7 || X == 10);
+    static constexpr bool kStores = !(X == 5 || X == 6);
+    static constexpr bool kSetPerm = X != 8;
+    static constexpr bool kArithSetup = X == 9 || X == 10;
+    static constexpr bool kPrio = X != 11;
+    static constexpr bool kReusePrep = X == 12;
+    static constexpr bool kStamp = X == 13;
+};
+#endif
+
+template <int MODE, bool RAGGED, bool TRAILER, class D>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
-    constexpr int DIAG = oct_diag_base(DIAGX);
-    constexpr bool kArithSetup = DIAGX == 9 || DIAGX == 10;
-    constexpr bool kPrio = kOctPrio && DIAGX != 11;
+    constexpr bool kPrio = kOctPrio && D::kPrio;
     constexpr int K = kOctK;
     constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
     constexpr int B = 2 * P;
     if (nq == 0) return;
-    const uint64_t t_start = DIAGX == 13 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t t_start = D::kStamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int nblocks = static_cast<int>((nq + 63u) >> 6);
     const uint32_t grp = lane >> 3;
     const int col = static_cast<int>(lane & 7u);
@@ -373,7 +393,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     int nres = 0;
     // store entries [kOctRes - nres, kOctRes)
     auto flush = [&]() __attribute__((always_inline)) {
-        if constexpr (DIAG == 5 || DIAG == 6) return;
+        if constexpr (!D::kStores) return;
         const int e0 = kOctRes - nres;
         const __amdgpu_buffer_rsrc_t os =
             MODE == kCompute
@@ -409,17 +429,15 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         const uint32_t set = fd & kFdSet;
         if (fd & kOctFirst) {  // set setup: this lane's packet is sorted position 8 set + grp
             const uint32_t ps = 8u * set + grp;
-            // DIAG 8: this lane's own block entry instead of the set's (no LDS round trip on the
-            // path to the loads; wrong results by design)
             uint32_t key, vrel, L;
-            if constexpr (kArithSetup) {
+            if constexpr (D::kArithSetup) {
                 L = p.ulen;
                 key = (((stream_words<MODE>(L) + 7u) >> 3) << 6) | ps;
                 vrel = ps * static_cast<uint32_t>(p.stride);
             } else {
-                key = DIAG == 8 ? LB.key : bperm(ps, LB.key);
-                vrel = DIAG == 8 ? LB.vrel : bperm(ps, LB.vrel);
-                L = DIAG == 8 ? LB.len : bperm(ps, LB.len);
+                key = D::kSetPerm ? bperm(ps, LB.key) : LB.key;
+                vrel = D::kSetPerm ? bperm(ps, LB.vrel) : LB.vrel;
+                L = D::kSetPerm ? bperm(ps, LB.len) : LB.len;
             }
             lreal = ps < static_cast<uint32_t>(__popcll(LB.mine));
             const uint32_t N = stream_words<MODE>(L);
@@ -441,7 +459,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         uint8_t *bb = p.base + boff;
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(bb, 0, static_cast<int>(readfirstlane_u32(LB.bend)), 0x00020000);
-        if constexpr (DIAG >= 2 && DIAG <= 4) {
+        if constexpr (!D::kLoads) {
 #pragma unroll
             for (int j = 0; j < K; ++j) S.u[j] = (o1 + 32u * j) * 0x9E3779B1u;
         } else {
@@ -488,7 +506,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
     // around a store in the ring)
     auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
-        if constexpr (DIAG == 5 || DIAG == 6) return;
+        if constexpr (!D::kStores) return;
         if (TRAILER && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
@@ -519,22 +537,22 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         const uint32_t fa = SA.fl, fb = SB.fl;
         constexpr uint32_t kFast = kOctHave | kOctUni | kOctFull;
         uint32_t accA = acc_c, accB = 0;
-        if ((DIAG == 0 || DIAG == 2 || DIAG == 6 || DIAG == 7 || DIAG == 8) && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
+        if (D::kRows && (fa & kFast) == kFast && (fb & (kFast | kOctFirst)) == (kFast | kOctFirst)) {
             if (fa & kOctFirst) oct_rows2<true>(SA, SB, accA, accB, hm, lds, c);
             else oct_rows2<false>(SA, SB, accA, accB, hm, lds, c);
         } else {
-            if (fa & kOctHave) accA = oct_frame<MODE, TRAILER, DIAG>(SA, accA, hm, lds, c);
-            if (fb & kOctHave) accB = oct_frame<MODE, TRAILER, DIAG>(SB, (fb & kOctFirst) ? 0u : accA, hm, lds, c);
+            if (fa & kOctHave) accA = oct_frame<MODE, TRAILER, D>(SA, accA, hm, lds, c);
+            if (fb & kOctHave) accB = oct_frame<MODE, TRAILER, D>(SB, (fb & kOctFirst) ? 0u : accA, hm, lds, c);
         }
         acc_c = (fb & kOctHave) ? accB : accA;
         uint32_t crcA = 0, crcB = 0;
         if (fa & fb & kOctLast) {  // both sets end here: the two final products interleave
-            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accA : final_mul(lds, accA, c.fin));
-            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accB : final_mul(lds, accB, c.fin));
+            crcA = ~group_xor<8>(D::kFinal ? final_mul(lds, accA, c.fin) : accA);
+            crcB = ~group_xor<8>(D::kFinal ? final_mul(lds, accB, c.fin) : accB);
         } else if (fa & kOctLast) {
-            crcA = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accA : final_mul(lds, accA, c.fin));
+            crcA = ~group_xor<8>(D::kFinal ? final_mul(lds, accA, c.fin) : accA);
         } else if (fb & kOctLast) {
-            crcB = ~group_xor<8>((DIAG == 1 || DIAG == 4 || DIAG == 5 || DIAG == 7) ? accB : final_mul(lds, accB, c.fin));
+            crcB = ~group_xor<8>(D::kFinal ? final_mul(lds, accB, c.fin) : accB);
         }
         inflight -= ((fa & kOctHave) ? 1 : 0) + ((fb & kOctHave) ? 1 : 0);
         // A's results (and its block's result store) before B's routing touches rbv: B may hold
@@ -559,8 +577,8 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                             : static_cast<uint64_t>(lo + q) * p.stride;
                 L = p.len ? m_len : p.ulen;
             }
-            if (DIAGX == 12 && !RAGGED && nb_next > 0 && (nb_next + 1) * 64 <= static_cast<int>(nq)) {
-                // DIAG 12 (strided, full blocks): the first block's preparation reused, only its
+            if (D::kReusePrep && !RAGGED && nb_next > 0 && (nb_next + 1) * 64 <= static_cast<int>(nq)) {
+                // (A/B, strided full blocks) the first block's preparation reused, only its
                 // position moved (what a free block schedule would leave)
                 NB.block = nb_next;
                 NB.boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(nb_next) * 64u) * p.stride;
@@ -621,7 +639,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             }
         }
     }
-    if constexpr (DIAGX == 13 && MODE == kCompute) {
+    if constexpr (D::kStamp && MODE == kCompute) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const __amdgpu_buffer_rsrc_t os =
             __builtin_amdgcn_make_buffer_rsrc(p.out ? p.out + lo : nullptr, 0, p.out ? static_cast<int>(nq * 4u) : 0, 0x00020000);
@@ -634,7 +652,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
 
 // The oct kernel's work for workgroup `bid` of `nblk` (its own kernel, or the short-packet
 // workgroups of the fused hybrid kernel below).
-template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
+template <int MODE, bool RAGGED, bool TRAILER, class D>
 __device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
     const uint32_t tw = nblk * kWavesPerGroup;
     // chunks of whole 64-packet blocks (whole-line result stores) unless that idles waves
@@ -660,13 +678,13 @@ __device__ __forceinline__ void oct_body(const BatchParams &p, uint4 *lds4, uint
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
-    run_oct<MODE, RAGGED, TRAILER, DIAG>(p, lds, c, lane, lo, nq);
+    run_oct<MODE, RAGGED, TRAILER, D>(p, lds, c, lane, lo, nq);
 }
 
-template <int MODE, bool RAGGED, bool TRAILER, int DIAG>
+template <int MODE, bool RAGGED, bool TRAILER, class D>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
-    oct_body<MODE, RAGGED, TRAILER, DIAG>(p, lds4, blockIdx.x, gridDim.x);
+    oct_body<MODE, RAGGED, TRAILER, D>(p, lds4, blockIdx.x, gridDim.x);
 }
 
 // The hybrid dispatch in ONE launch: workgroups [0, g_oct) are the oct kernel's (L < split_len),
@@ -677,7 +695,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams 
 template <int MODE, bool TRAILER, bool COMPACT>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_kernel(BatchParams p, uint32_t g_oct) {
     __shared__ uint4 lds4[kLdsBytes / 16];
-    if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, 0>(p, lds4, blockIdx.x, g_oct);
+    if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, OctProduct>(p, lds4, blockIdx.x, g_oct);
     else long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
 }
 
@@ -689,26 +707,26 @@ uint32_t oct_max_len() { return kOctMaxL; }
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool ragged = p.off != nullptr || p.len != nullptr;
-#define ICRC_O(M, R, T, G) hipLaunchKernelGGL((icrc_oct_kernel<M, R, T, G>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#define ICRC_O(M, R, T, D) hipLaunchKernelGGL((icrc_oct_kernel<M, R, T, D>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p)
+#ifdef ICRC_AB_BUILD  // the ablations (wrong results by design): the A/B library only
 #define ICRC_OD(M, R)                                                \
     do {                                                             \
         switch (diag) {                                              \
-        case 1: ICRC_O(M, R, false, 1); break;                       \
-        case 2: ICRC_O(M, R, false, 2); break;                       \
-        case 3: ICRC_O(M, R, false, 3); break;                       \
-        case 4: ICRC_O(M, R, false, 4); break;                       \
-        case 5: ICRC_O(M, R, false, 5); break;                       \
-        case 6: ICRC_O(M, R, false, 6); break;                       \
-        case 7: ICRC_O(M, R, false, 7); break;                       \
-        case 9: ICRC_O(M, R, false, 9); break;                       \
-        case 10: ICRC_O(M, R, false, 10); break;                     \
-        case 11: ICRC_O(M, R, false, 11); break;                     \
-        case 12: ICRC_O(M, R, false, 12); break;                     \
-        case 13: ICRC_O(M, R, false, 13); break;                     \
-        default: ICRC_O(M, R, false, 8); break;                      \
+        case 1: ICRC_O(M, R, false, OctAblation<1>); break;          \
+        case 2: ICRC_O(M, R, false, OctAblation<2>); break;          \
+        case 3: ICRC_O(M, R, false, OctAblation<3>); break;          \
+        case 4: ICRC_O(M, R, false, OctAblation<4>); break;          \
+        case 5: ICRC_O(M, R, false, OctAblation<5>); break;          \
+        case 6: ICRC_O(M, R, false, OctAblation<6>); break;          \
+        case 7: ICRC_O(M, R, false, OctAblation<7>); break;          \
+        case 9: ICRC_O(M, R, false, OctAblation<9>); break;          \
+        case 10: ICRC_O(M, R, false, OctAblation<10>); break;        \
+        case 11: ICRC_O(M, R, false, OctAblation<11>); break;        \
+        case 12: ICRC_O(M, R, false, OctAblation<12>); break;        \
+        case 13: ICRC_O(M, R, false, OctAblation<13>); break;        \
+        default: ICRC_O(M, R, false, OctAblation<8>); break;         \
         }                                                            \
     } while (0)
-#ifdef ICRC_AB_BUILD  // diagnostics 41-46 (wrong results by design): the A/B library only
 #define ICRC_OM_DIAG(M)                                              \
         if (diag != 0 && M == kCompute && !p.trailer) {              \
             if (ragged) ICRC_OD(M, true);                            \
@@ -721,18 +739,20 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
     do {                                                             \
         ICRC_OM_DIAG(M)                                              \
         if (ragged) {                                                \
-            if (p.trailer) ICRC_O(M, true, true, 0);                 \
-            else ICRC_O(M, true, false, 0);                          \
+            if (p.trailer) ICRC_O(M, true, true, OctProduct);        \
+            else ICRC_O(M, true, false, OctProduct);                 \
         } else {                                                     \
-            if (p.trailer) ICRC_O(M, false, true, 0);                \
-            else ICRC_O(M, false, false, 0);                         \
+            if (p.trailer) ICRC_O(M, false, true, OctProduct);       \
+            else ICRC_O(M, false, false, OctProduct);                \
         }                                                            \
     } while (0)
     if (mode == kCompute) ICRC_OM(kCompute);
     else ICRC_OM(kVerify);
 #undef ICRC_OM
 #undef ICRC_OM_DIAG
+#ifdef ICRC_AB_BUILD
 #undef ICRC_OD
+#endif
 #undef ICRC_O
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }

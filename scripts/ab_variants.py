@@ -73,6 +73,19 @@ def main():
                 name = f"W{w3.n}"
             jobs[name] = (rt, nb3, out3)
             continue
+        if name in ("C2short", "C2long"):  # the C2 batch's own packets of one half only (same buffer, same
+            # offsets): L <= 1088 (the oct half) / L >= 1089 (the long-packet half) — the mix decomposition
+            w2 = workloads.mixed_mtu_stream(4 << 20)
+            b2 = workloads.synthesize(eng, w2, stream=s)
+            sel = (w2.lens <= 1088) if name == "C2short" else (w2.lens >= 1089)
+            off_s, len_s = np.ascontiguousarray(w2.off[sel]), np.ascontiguousarray(w2.lens[sel])
+            o2, l2 = dev(off_s), dev(len_s)
+            out2 = torch.zeros(int(sel.sum()), dtype=torch.int32, device="cuda")
+            keep += [b2, o2, l2, out2]
+            jobs[name] = (lambda b2=b2, o2=o2, l2=l2, out2=out2, n=int(sel.sum()): eng.compute_batch(
+                b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), n, out2.data_ptr(), False, 0, s),
+                int(len_s.astype(np.uint64).sum()), out2)
+            continue
         kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0),
               "C2m": dict(classes=(256, 1024)), "C2snr": dict(classes=(256,), ragged_frac=0.0)}[name]
         w2 = workloads.mixed_mtu_stream(4 << 20, **kw)

@@ -1,0 +1,33 @@
+#!/bin/bash
+# scripts/gpu_r04_probe.sh — one gpurun call: the submitter's message rate from 1-4 threads
+# (scripts/_build/msg_probe, C++), then the C2 mix decomposition (scripts/ab_variants.py, default
+# dispatch).  Every GPU step has its own time limit; a crash / timeout stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+stop_if_fatal() { case "$1" in 0) ;; *) echo "FATAL: $2 exited $1 — stopping"; exit "$1";; esac; }
+if [ -n "${TESTK:-}" ]; then  # a subset of the GPU tests first (pytest -k expression)
+  timeout -k 10 600 python -u -m pytest tests -q -m gpu -x -k "$TESTK" --timeout 120 --timeout-method thread \
+    > $OUT/gpu_tests_sub.log 2>&1; rc=$?
+  tail -3 $OUT/gpu_tests_sub.log; stop_if_fatal $rc tests
+fi
+if [ "${PLACE:-0}" = 1 ]; then
+  timeout -k 10 600 python3 -u scripts/probe_packetize_place.py > $OUT/pk_place.jsonl 2> $OUT/pk_place.err; rc=$?
+  cat $OUT/pk_place.jsonl; tail -3 $OUT/pk_place.err; stop_if_fatal $rc probe_packetize_place
+fi
+if [ "${SPLIT:-0}" = 1 ]; then
+  timeout -k 10 600 python3 -u scripts/probe_split.py > $OUT/c2_split.jsonl 2> $OUT/c2_split.err; rc=$?
+  cat $OUT/c2_split.jsonl; tail -3 $OUT/c2_split.err; stop_if_fatal $rc probe_split
+fi
+if [ "${MSG:-1}" = 1 ]; then
+  LD_LIBRARY_PATH=open-rdma-driver_amd/_build timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 2 3 4 \
+    > $OUT/msg_threads.jsonl 2> $OUT/msg_threads.err; rc=$?
+  cat $OUT/msg_threads.jsonl; stop_if_fatal $rc msg_probe
+fi
+if [ "${DECOMP:-1}" = 1 ]; then
+  JOBS=${JOBS:-C2,C2short,C2long,C2nr,C2s,C2snr,C2k,C2m,S316} ROUNDS=${ROUNDS:-3} timeout -k 10 600 \
+    python3 -u scripts/ab_variants.py ${VARIANTS:--1} > $OUT/c2_decomp.jsonl 2> $OUT/c2_decomp.err; rc=$?
+  cat $OUT/c2_decomp.jsonl; tail -3 $OUT/c2_decomp.err; stop_if_fatal $rc ab_variants
+fi
+echo "== done"

@@ -10,9 +10,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "icrc.h"
@@ -57,6 +60,61 @@ void run(const char *name, uint8_t *buf, uint32_t npk, uint32_t L, int calls) {
     fflush(stdout);
 }
 
+// T threads, each its own pinned (or pageable) copy of the message, each running `calls` messages
+// (compute + verify): messages/s in total and p50 / p99 per message — the emulator's three callers.
+void run_threads(const char *name, const std::vector<uint8_t> &src, bool pinned_bufs, uint32_t npk, uint32_t L,
+                 int calls, int T) {
+    std::vector<uint8_t *> bufs(T);
+    std::vector<std::vector<uint8_t>> pageable(T);
+    for (int t = 0; t < T; ++t) {
+        if (pinned_bufs) {
+            if (hipHostMalloc(reinterpret_cast<void **>(&bufs[t]), src.size(), hipHostMallocDefault) != hipSuccess) {
+                fprintf(stderr, "hipHostMalloc failed\n");
+                exit(1);
+            }
+        } else {
+            pageable[t] = src;
+            bufs[t] = pageable[t].data();
+        }
+        std::memcpy(bufs[t], src.data(), src.size());
+    }
+    std::vector<std::vector<double>> lat(T);
+    std::atomic<long> bad{0};
+    std::atomic<int> ready{0};
+    auto worker = [&](int t) {
+        std::vector<uint64_t> off(npk);
+        std::vector<uint32_t> len(npk, L), crc(npk);
+        std::vector<uint8_t> ok(npk);
+        for (uint32_t i = 0; i < npk; ++i) off[i] = static_cast<uint64_t>(i) * L;
+        ready.fetch_add(1);
+        while (ready.load() < T) {
+        }
+        for (int c = 0; c < calls + 20; ++c) {
+            const auto t0 = clk::now();
+            const int r1 = icrc_compute_batch(bufs[t], off.data(), len.data(), npk, crc.data(), 1);
+            const int r2 = icrc_verify_batch(bufs[t], off.data(), len.data(), npk, ok.data(), 1);
+            const auto t1 = clk::now();
+            long b = (r1 || r2) ? 1 : 0;
+            for (uint32_t i = 0; i < npk; ++i) b += ok[i] != ICRC_VERIFY_OK;
+            if (b) bad.fetch_add(b);
+            if (c >= 20) lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+        }
+    };
+    const auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(worker, t);
+    for (auto &x : th) x.join();
+    const double secs = std::chrono::duration<double>(clk::now() - t0).count();
+    std::vector<double> all;
+    for (auto &v : lat) all.insert(all.end(), v.begin(), v.end());
+    printf("{\"case\": \"%s\", \"threads\": %d, \"packets\": %u, \"packet_bytes\": %u, \"messages_per_s\": %.0f, "
+           "\"message_p50_us\": %.1f, \"message_p99_us\": %.1f, \"bad\": %ld}\n",
+           name, T, npk, L, T * (calls + 20) / secs, pct(all, 0.5), pct(all, 0.99), bad.load());
+    fflush(stdout);
+    if (pinned_bufs)
+        for (auto *b : bufs) (void)hipHostFree(b);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -76,6 +134,15 @@ int main(int argc, char **argv) {
         return 1;
     }
     std::memcpy(pinned, pageable.data(), pageable.size());
+    if (argc > 2) {  // msg_probe CALLS THREADS...: the multi-threaded message rate only
+        for (int a = 2; a < argc; ++a) {
+            const int T = atoi(argv[a]);
+            run_threads("pinned", pageable, true, npk, L, calls, T);
+            run_threads("pageable", pageable, false, npk, L, calls, T);
+        }
+        (void)hipHostFree(pinned);
+        return 0;
+    }
     run("pinned", pinned, npk, L, calls);
     run("pageable", pageable.data(), npk, L, calls);
     run("pinned_1_packet", pinned, 1, L, calls);

@@ -18,6 +18,9 @@ import sys
 from collections import defaultdict
 
 N, L = 1 << 20, 4156
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_source_hash  # noqa: E402  (sha of the kernel sources this summary describes)
 
 
 def short(name):
@@ -84,7 +87,7 @@ def main():
             write = d.get("WRITE_SIZE_KB_mean", 0.0) * 1024.0
             alg = N * L
             res["icrc_traffic_per_launch"] = {
-                "kernel": name, "packets": N, "packet_bytes": L,
+                "kernel": name, "packets": N, "packet_bytes": L, "source_hash": kernel_source_hash(),
                 "fetch_bytes_counted": d["FETCH_SIZE_KB_mean"] * 1024.0,
                 "fetch_correction": round(corr, 4), "fetch_bytes_corrected": round(fetch),
                 "write_bytes": round(write), "traffic_bytes": round(fetch + write),
