@@ -176,6 +176,17 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     // Default: both halves in one launch (the fused hybrid kernel).  A forced hybrid variant
     // (100 + q, 200 + q: A/B) keeps the two-stream fork / join below.
     if (!hybrid_forced) {
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_HYBRID_SEQ = 1: the two halves as two kernels one after the other on the
+        // caller's stream (oct, then long-packet); 2: long-packet first
+        if (const char *v = std::getenv("ICRC_AB_HYBRID_SEQ")) {
+            const int seq = std::atoi(v);
+            if (seq == 1 || seq == 2) {
+                int rc = seq == 1 ? icrc::launch_batch(mode, p, grid, stream) : icrc::launch_long(mode, p, grid, stream);
+                if (rc == ICRC_OK) rc = seq == 1 ? icrc::launch_long(mode, p, grid, stream) : icrc::launch_batch(mode, p, grid, stream);
+                return rc;
+            }
+        }
+#endif
         int grid_long = grid;
 #ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_LONG_GRID = long-packet workgroups per oct workgroup
         static const int long_mult = [] {
@@ -1063,10 +1074,6 @@ int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t s
     p.pkt_len = d_pkt_len;
     p.icrc = d_icrc;
     p.table = e->d_table;
-    p.rotate = 1;
-#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK_ROT=0 walks every wave's chunk in order
-    if (const char *v = std::getenv("ICRC_AB_PK_ROT")) p.rotate = static_cast<uint32_t>(std::atoi(v));
-#endif
     return icrc::launch_packetize(p, grid_for(e, npackets), stream);
 }
 

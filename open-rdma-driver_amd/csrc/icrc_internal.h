@@ -96,7 +96,7 @@ constexpr int kRxVariantBase = 300;
 // library (built with ICRC_AB_BUILD: _build/libicrc_amd_ab.so, for measurement scripts and the
 // bench's loads-only denominator) adds the quad kernels 20, 24-26 (icrc_quad.hip) and the
 // diagnostics 15, 18, 19, 21, 22, 31, 32, 35, 41-53, whose results are wrong by design (49 and 51 are
-// exact on strided batches only / on all batches, but ablations all the same).
+// exact on strided batches only / on all batches, 48, 52 and 53 exact, but ablations all the same).
 #ifdef ICRC_AB_BUILD
 inline bool is_batch_variant(int v) {
     switch (v) {
@@ -137,7 +137,7 @@ uint32_t oct_max_len();
 int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);
 // The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
 // short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
-inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 8 ? oct_max_len() + 1u : kSplitLen; }
+inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 13 ? oct_max_len() + 1u : kSplitLen; }
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {
@@ -151,7 +151,6 @@ struct PacketizeParams {
     uint32_t *pkt_len;
     uint32_t *icrc;
     const uint32_t *table;
-    uint32_t rotate;  // 1: each wave starts its chunk at a hashed packet and wraps (default); 0: in order (A/B)
 };
 int launch_packetize(const PacketizeParams &p, int grid, void *stream);
 int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, uint8_t *out, uint32_t stride,

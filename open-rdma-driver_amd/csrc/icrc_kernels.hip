@@ -469,8 +469,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                                                                           const icrc_write_msg *msgs, uint32_t nmsgs,
                                                                           uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
                                                                           uint32_t *pkt_len,
-                                                                          uint32_t *icrc_out, const uint32_t *table,
-                                                                          uint32_t rotate) {
+                                                                          uint32_t *icrc_out, const uint32_t *table) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     table_fill(lds4, table);
     const char *lds = reinterpret_cast<const char *>(lds4);
@@ -487,29 +486,22 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t hi = (npk - lo) < chunk ? npk : lo + chunk;
 
-    // The wave walks its chunk starting at a hashed packet and wrapping around, so that the 4096
-    // waves' read and write streams (chunks a fixed number of bytes apart) do not advance through
-    // the memory channels in lockstep, whatever the buffers' physical placement.
-    const uint32_t n = hi - lo;
-    const uint32_t rot = rotate ? ((gw * 2654435761u) >> 7) % n : 0u;
+    // message holding packet lo: binary search on first_packet
+    int mlo = 0, mhi = static_cast<int>(nmsgs) - 1;
+    while (mlo < mhi) {
+        const int mid = (mlo + mhi + 1) >> 1;
+        if (msg_first_packet(msgs, mid) <= lo) mlo = mid;
+        else mhi = mid - 1;
+    }
+    mlo = __builtin_amdgcn_readfirstlane(mlo);
 
-    // message holding packet pk: binary search on first_packet
-    auto find_msg = [&](uint32_t pk) __attribute__((always_inline)) -> int {
-        int a = 0, b = static_cast<int>(nmsgs) - 1;
-        while (a < b) {
-            const int mid = (a + b + 1) >> 1;
-            if (msg_first_packet(msgs, mid) <= pk) a = mid;
-            else b = mid - 1;
-        }
-        return __builtin_amdgcn_readfirstlane(a);
-    };
-    int mlo = find_msg(lo + rot);
-    const int mwrap = rot ? find_msg(lo) : mlo;
-
-    // load side: one message cursor; the plan of packet pk (or an empty slot past the chunk)
+    // load side: one message cursor; the plan of packet pk (or an empty slot past hi).  (Walking
+    // each wave's chunk from a hashed start instead, so that the waves' streams do not advance in
+    // lockstep, measured the same at every relative placement of d_src and d_wire:
+    // profiles/r04_packetize_placement_rotation.jsonl.)
     MsgRegs lm;
     lm.idx = -1;
-    uint32_t next_t = 0;  // packets of the chunk issued so far; the next is lo + (next_t + rot) mod n
+    uint32_t next_pk = lo;
     bool slow_seen = false;
     auto locate = [&](MsgRegs &m, uint32_t pk, SendPlan &g) __attribute__((always_inline)) {
         while (m.idx < static_cast<int>(nmsgs) && (m.idx < 0 || pk >= msg_u32(m, kMFirst) + msg_u32(m, kMNpk)))
@@ -524,14 +516,9 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     // next packet of the ring (fast packets only), its header lanes and its row loads
     auto fill = [&](SendPlan &g, uint32_t &hvec, uint32_t (&u)[kRows]) __attribute__((always_inline)) {
         plan_empty(g);
-        while (next_t < n) {
-            const uint32_t t = next_t + rot;
-            if (t == n) {  // wrapped to the chunk's first packet: restart the message cursor there
-                lm.idx = -1;
-                mlo = mwrap;
-            }
-            locate(lm, lo + (t >= n ? t - n : t), g);
-            ++next_t;
+        while (next_pk < hi) {
+            locate(lm, next_pk, g);
+            ++next_pk;
             if (g.fast) break;
             slow_seen = true;
             plan_empty(g);
@@ -630,7 +617,6 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
     if (slow_seen) {
         MsgRegs sm;
         sm.idx = -1;
-        mlo = mwrap;
         for (uint32_t pk = lo; pk < hi; ++pk) {
             SendPlan sg;
             locate(sm, pk, sg);
@@ -964,7 +950,7 @@ int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((icrc_packetize_kernel<1>), dim3(grid), dim3(kThreadsPerGroup), 0,
                        static_cast<hipStream_t>(stream), p.src, p.src_bytes, p.msgs, p.nmsgs, p.npackets, p.wire,
-                       p.wire_bytes, p.pkt_len, p.icrc, p.table, p.rotate);
+                       p.wire_bytes, p.pkt_len, p.icrc, p.table);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -36,6 +36,8 @@
 // per-packet tail loop.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "icrc_device.h"
 #include "icrc_internal.h"
 #include "icrc_long.h"
@@ -449,6 +451,10 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         }
         const uint32_t lf = (fd >> 16) & 0xFFu;
         const uint32_t fo = 32u * K * lf;
+        // (Rows past a shorter packet's end in a set of mixed row counts re-read the bytes after it:
+        // those are the block's next packets, which the same wave reads soon after, so the
+        // over-read acts as their L2 prefetch — skipping the frames past a lane's own packet
+        // measured no faster, profiles/r04_ab_oct_frame_skip_rejected.jsonl.)
         const bool live = have && lreal;
         const uint32_t o0 = (live && lkf + 8 * K * static_cast<int>(lf) >= 1) ? lvrow0 + fo : kOctOOR;
         const uint32_t o1 = live ? lvrow0 + 32u + fo : kOctFar;  // rows >= 1: + 32 (j - 1) immediate

@@ -20,13 +20,17 @@ if [ "${SPLIT:-0}" = 1 ]; then
   timeout -k 10 600 python3 -u scripts/probe_split.py > $OUT/c2_split.jsonl 2> $OUT/c2_split.err; rc=$?
   cat $OUT/c2_split.jsonl; tail -3 $OUT/c2_split.err; stop_if_fatal $rc probe_split
 fi
+if [ -n "${AB_ENV:-}" ]; then
+  timeout -k 10 600 python3 -u scripts/probe_env_ab.py > $OUT/env_ab.jsonl 2> $OUT/env_ab.err; rc=$?
+  cat $OUT/env_ab.jsonl; tail -3 $OUT/env_ab.err; stop_if_fatal $rc probe_env_ab
+fi
 if [ "${MSG:-1}" = 1 ]; then
   LD_LIBRARY_PATH=open-rdma-driver_amd/_build timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 2 3 4 \
     > $OUT/msg_threads.jsonl 2> $OUT/msg_threads.err; rc=$?
   cat $OUT/msg_threads.jsonl; stop_if_fatal $rc msg_probe
 fi
 if [ "${DECOMP:-1}" = 1 ]; then
-  JOBS=${JOBS:-C2,C2short,C2long,C2nr,C2s,C2snr,C2k,C2m,S316} ROUNDS=${ROUNDS:-3} timeout -k 10 600 \
+  JOBS=${DJOBS:-C2,C2short,C2long,C2nr,C2s,C2snr,C2k,C2m,S316} ROUNDS=${ROUNDS:-3} timeout -k 10 600 \
     python3 -u scripts/ab_variants.py ${VARIANTS:--1} > $OUT/c2_decomp.jsonl 2> $OUT/c2_decomp.err; rc=$?
   cat $OUT/c2_decomp.jsonl; tail -3 $OUT/c2_decomp.err; stop_if_fatal $rc ab_variants
 fi
