@@ -385,8 +385,7 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
 
 PMC_TRAFFIC_FILE = "r04_pmc_traffic.json"
 # the sources the C1 kernel is built from: a traffic summary taken on another build is not this one's
-KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp",
-                  "icrc_capi.cpp")
+KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp")
 
 
 def kernel_source_hash() -> str:
@@ -757,6 +756,16 @@ def host_message_c0(eng, stream, args):
                 "failed_verifies": int(sum(bad)), "packets_per_message": int(w.n), "message_bytes": nbytes}
     out["c0_message_note"] = ("per message: icrc_compute_batch(write_trailer=1) + icrc_verify_batch(zero_trailer=1) on "
                               "a 64 x 4156-B WRITE in host memory; compare cpu_context.c0_roundtrip_1_core")
+    # The same calls from native threads (scripts/_build/msg_probe, C++: the reference's callers are
+    # Rust threads; Python threads serialise on the GIL around every ctypes call), 1 and 3 threads.
+    probe = os.path.join(ROOT, "scripts", "_build", "msg_probe")
+    if os.path.exists(probe):
+        env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(icrc_amd.LIB_PATH))
+        try:
+            r = subprocess.run([probe, "1000", "1", "3"], capture_output=True, text=True, timeout=180, env=env)
+            out["c0_message_native"] = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+        except (subprocess.TimeoutExpired, ValueError) as e:
+            out["c0_message_native"] = f"msg_probe failed: {e}"
     return out
 
 

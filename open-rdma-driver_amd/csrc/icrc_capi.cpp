@@ -138,7 +138,12 @@ int grid_for(const icrc_engine *e, uint32_t n);
 int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     // spread (small host-mapped batches): one workgroup per packet up to #CUs, so that as many CUs
     // as possible read host memory over PCIe at once
-    const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>(p.n, 1u), static_cast<uint32_t>(e->num_cu)))
+    uint32_t spread_per_wg = 1;  // packets per workgroup of a spread launch
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_SPREAD = packets per workgroup of a spread (small host-mapped) launch
+    if (const char *v = std::getenv("ICRC_AB_SPREAD")) spread_per_wg = std::max(1, std::min(16, std::atoi(v)));
+#endif
+    const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>((p.n + spread_per_wg - 1) / spread_per_wg, 1u),
+                                                                    static_cast<uint32_t>(e->num_cu)))
                               : grid_for(e, p.n);
     p.split_len = 0;
 #ifdef ICRC_AB_BUILD  // A/B: the persistent waves' work skew (BatchParams::skew), read per call:

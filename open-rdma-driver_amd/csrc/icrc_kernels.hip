@@ -464,7 +464,9 @@ __device__ __forceinline__ void send_record(SendResults &r, uint32_t *pkt_len, u
     }
 }
 
-template <int D>
+// D: packets whose payload rows are in flight while one is processed; LAUX / SAUX: cache policy of
+// the payload loads / wire stores (0 default, 2 nt).  The product runs <1, 0, 0>.
+template <int D, int LAUX = 0, int SAUX = 0>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const uint8_t *src, uint64_t src_bytes,
                                                                           const icrc_write_msg *msgs, uint32_t nmsgs,
                                                                           uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
 #pragma unroll
         for (int j = 0; j < kRows; ++j) {
             const int o = vb + 256 * j;
-            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, o >= 0 ? o : static_cast<int>(kSendOOR), 0, 0);
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, o >= 0 ? o : static_cast<int>(kSendOOR), 0, LAUX);
         }
     };
 
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
                 const int keep = static_cast<int>(room) - 4 * pw;
                 w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
-            __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, SAUX);
             const uint32_t uu = w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u));
             acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
         }
@@ -948,9 +950,24 @@ int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, ui
 int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
     if (p.npackets == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((icrc_packetize_kernel<1>), dim3(grid), dim3(kThreadsPerGroup), 0,
-                       static_cast<hipStream_t>(stream), p.src, p.src_bytes, p.msgs, p.nmsgs, p.npackets, p.wire,
-                       p.wire_bytes, p.pkt_len, p.icrc, p.table);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define ICRC_PK(D, LA, SA)                                                                                          \
+    hipLaunchKernelGGL((icrc_packetize_kernel<D, LA, SA>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p.src, p.src_bytes, \
+                       p.msgs, p.nmsgs, p.npackets, p.wire, p.wire_bytes, p.pkt_len, p.icrc, p.table)
+#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK = 0 the product shape; 1: two packets in flight; 2: nt wire stores;
+    // 3: nt payload loads; 4: nt loads and stores
+    const char *v = std::getenv("ICRC_AB_PK");
+    switch (v ? std::atoi(v) : 0) {
+    case 1: ICRC_PK(2, 0, 0); break;
+    case 2: ICRC_PK(1, 0, 2); break;
+    case 3: ICRC_PK(1, 2, 0); break;
+    case 4: ICRC_PK(1, 2, 2); break;
+    default: ICRC_PK(1, 0, 0); break;
+    }
+#else
+    ICRC_PK(1, 0, 0);
+#endif
+#undef ICRC_PK
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -24,6 +24,14 @@ if [ -n "${AB_ENV:-}" ]; then
   timeout -k 10 600 python3 -u scripts/probe_env_ab.py > $OUT/env_ab.jsonl 2> $OUT/env_ab.err; rc=$?
   cat $OUT/env_ab.jsonl; tail -3 $OUT/env_ab.err; stop_if_fatal $rc probe_env_ab
 fi
+if [ -n "${SPREAD_VALUES:-}" ]; then  # msg_probe on the A/B library, one run per ICRC_AB_SPREAD value
+  mkdir -p /tmp/icrc_ablib && ln -sf "$PWD/open-rdma-driver_amd/_build/libicrc_amd_ab.so" /tmp/icrc_ablib/libicrc_amd.so
+  for v in $SPREAD_VALUES; do
+    ICRC_AB_SPREAD=$v LD_LIBRARY_PATH=/tmp/icrc_ablib timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 3 4 \
+      > $OUT/msg_spread_$v.jsonl 2> $OUT/msg_spread_$v.err; rc=$?
+    sed "s/^{/{\"spread_per_wg\": $v, /" $OUT/msg_spread_$v.jsonl; stop_if_fatal $rc msg_probe_spread
+  done
+fi
 if [ "${MSG:-1}" = 1 ]; then
   LD_LIBRARY_PATH=open-rdma-driver_amd/_build timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 2 3 4 \
     > $OUT/msg_threads.jsonl 2> $OUT/msg_threads.err; rc=$?

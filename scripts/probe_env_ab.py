@@ -30,6 +30,23 @@ def main():
            "C2nr": dict(ragged_frac=0.0)}
     jobs = {}
     for name in os.environ.get("JOBS", "C2,C2m").split(","):
+        if name == "PK":  # the fused send packetizer: 192 x 16 MiB WRITE -> 786 K x 4156-B packets
+            MSG, SLOT = 16 << 20, 28 + 28 + 4096 + 4
+            specs = [dict(local_va=0x7F0000000000 + i * MSG, remote_va=0x7E0000000000 + i * MSG, payload_offset=i * MSG,
+                          total_len=MSG, pmtu=4096, rkey=0x2000003, dqpn=2 + i, psn=0, msn=i & 0xFFFF,
+                          dst_ip=0xC0A80003, kind=0) for i in range(192)]
+            msgs = icrc_amd.write_messages(specs, slot_stride=SLOT)
+            npk = int(msgs["npackets"].sum())
+            d_src = torch.randint(0, 256, (192 * MSG,), dtype=torch.uint8, device="cuda")
+            d_wire = torch.empty(npk * SLOT, dtype=torch.uint8, device="cuda")
+            d_msgs = dev(msgs.view(np.uint8))
+            d_len = torch.zeros(npk, dtype=torch.int32, device="cuda")
+            d_icrc = torch.zeros(npk, dtype=torch.int32, device="cuda")
+            jobs[name] = (lambda d_src=d_src, d_wire=d_wire, d_msgs=d_msgs, d_len=d_len, d_icrc=d_icrc, npk=npk:
+                          eng.packetize(d_src.data_ptr(), d_src.numel(), d_msgs.data_ptr(), 192, npk, d_wire.data_ptr(),
+                                        d_wire.numel(), d_len.data_ptr(), d_icrc.data_ptr(), s),
+                          npk * (4096 + 4156 + 8), d_icrc, (d_src, d_wire, d_msgs, d_len))
+            continue
         if name == "S316":
             w = workloads.write_middle_stream(1 << 22, pmtu=256)
             L = int(w.lens[0])
