@@ -199,6 +199,12 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
             return v ? std::max(1, std::atoi(v)) : 1;
         }();
         grid_long = grid * long_mult;
+        // ICRC_AB_LONG_CUS = k: k CUs run long-packet workgroups from the start (grid - k oct
+        // workgroups, k long ones), instead of the long half waiting for oct workgroups to retire
+        if (const char *v = std::getenv("ICRC_AB_LONG_CUS")) {
+            const int k = std::atoi(v);
+            if (k > 0 && k < grid) return icrc::launch_hybrid(mode, p, grid - k, k, stream);
+        }
 #endif
         return icrc::launch_hybrid(mode, p, grid, grid_long, stream);
     }

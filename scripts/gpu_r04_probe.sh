@@ -32,6 +32,10 @@ if [ -n "${SPREAD_VALUES:-}" ]; then  # msg_probe on the A/B library, one run pe
     sed "s/^{/{\"spread_per_wg\": $v, /" $OUT/msg_spread_$v.jsonl; stop_if_fatal $rc msg_probe_spread
   done
 fi
+if [ "${PRESORT:-0}" = 1 ]; then
+  timeout -k 10 600 python3 -u scripts/probe_presort.py > $OUT/presort.jsonl 2> $OUT/presort.err; rc=$?
+  cat $OUT/presort.jsonl; tail -3 $OUT/presort.err; stop_if_fatal $rc probe_presort
+fi
 if [ "${MSG:-1}" = 1 ]; then
   LD_LIBRARY_PATH=open-rdma-driver_amd/_build timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 2 3 4 \
     > $OUT/msg_threads.jsonl 2> $OUT/msg_threads.err; rc=$?
