@@ -36,6 +36,15 @@ if [ "${PRESORT:-0}" = 1 ]; then
   timeout -k 10 600 python3 -u scripts/probe_presort.py > $OUT/presort.jsonl 2> $OUT/presort.err; rc=$?
   cat $OUT/presort.jsonl; tail -3 $OUT/presort.err; stop_if_fatal $rc probe_presort
 fi
+if [ "${MSGAB:-0}" = 1 ]; then  # the round-3 library (one launch in flight) vs this build, alternating
+  for r in 1 2; do
+    for b in old_r03 new; do
+      d=open-rdma-driver_amd/_build; [ $b = old_r03 ] && d=open-rdma-driver_amd/_build/old_r03
+      LD_LIBRARY_PATH=$d timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 3 > $OUT/msgab_$b.jsonl 2> $OUT/msgab_$b.err; rc=$?
+      sed "s/^{/{\"build\": \"$b\", \"round\": $r, /" $OUT/msgab_$b.jsonl; stop_if_fatal $rc msg_probe_ab
+    done
+  done
+fi
 if [ "${MSG:-1}" = 1 ]; then
   LD_LIBRARY_PATH=open-rdma-driver_amd/_build timeout -k 10 240 scripts/_build/msg_probe ${CALLS:-2000} 1 2 3 4 \
     > $OUT/msg_threads.jsonl 2> $OUT/msg_threads.err; rc=$?
