@@ -28,13 +28,15 @@
  *   - The caller owns every buffer.  Synchronous calls retain no pointer; *_device calls
  *     borrow their pointers until the stream they were issued on is synchronised.
  *   - All entry points are reentrant.  Scalar calls, and host batches of at most 1024 packets and
- *     8 MiB (one message: configs[0] is 64 x 4156 B), queue on the engine's combining submitter:
- *     the kernel reads the packets from pinned, device-mapped host memory (the caller's own
- *     buffer when it is pinned, else a copy in a staging slot of the calling thread), and
- *     concurrent callers are merged into one launch (one thread launches, the others wait for
- *     their results).  Larger host batches serialise per engine on its two pipelined H2D staging
- *     buffers; device batches only enqueue on the caller's stream.  The default-engine registry
- *     is lock-protected.
+ *     8 MiB (one message: configs[0] is 64 x 4156 B), queue on the engine's submitter: the kernel
+ *     reads the packets from pinned, device-mapped host memory (the caller's own buffer when the
+ *     whole span lies in one pinned allocation and every packet is 4-byte aligned, else a copy in
+ *     a staging slot of the calling thread).  The submitter has four launch lanes (a stream each):
+ *     a caller that finds a free lane launches its call there and waits on that stream only, so up
+ *     to four calls are in flight at once (the emulator's three threads each get one); callers
+ *     that find every lane busy are merged into the next launch.  Larger host batches serialise
+ *     per engine on its two pipelined H2D staging buffers; device batches only enqueue on the
+ *     caller's stream.  The default-engine registry is lock-protected.
  *   - Every CRC is computed by the HIP kernel on the GPU; there is no CPU fallback.  With
  *     no usable GPU the calls return ICRC_ENODEV.
  */
