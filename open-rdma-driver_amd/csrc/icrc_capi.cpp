@@ -127,6 +127,36 @@ struct DeviceGuard {
 
 int grid_for(const icrc_engine *e, uint32_t n);
 
+// Dispatch knobs.  The product runs the defaults; the A/B library (ICRC_AB_BUILD) reads them from
+// the environment on every call, so that one process can time the alternatives on one box (the
+// records of each are under profiles/).
+struct DispatchKnobs {
+    uint32_t spread_per_wg = 1;  // ICRC_AB_SPREAD: packets per workgroup of a spread launch
+    int skew = -1, skew_oct = -1, skew_long = -1;  // ICRC_AB_SKEW[_OCT|_LONG]: the waves' work skew
+    uint32_t split = 0;          // ICRC_AB_SPLIT: the length split of ragged batches (0: the variant's)
+    int hybrid_seq = 0;          // ICRC_AB_HYBRID_SEQ: 1 / 2 = the halves as two kernels in a row (oct / long first)
+    int long_grid_mult = 1;      // ICRC_AB_LONG_GRID: long-packet workgroups per oct workgroup
+    int long_cus = 0;            // ICRC_AB_LONG_CUS: CUs running long-packet workgroups from the start
+};
+DispatchKnobs dispatch_knobs() {
+    DispatchKnobs k;
+#ifdef ICRC_AB_BUILD
+    auto env = [](const char *name, int dflt) {
+        const char *v = std::getenv(name);
+        return v ? std::atoi(v) : dflt;
+    };
+    k.spread_per_wg = static_cast<uint32_t>(std::max(1, std::min(16, env("ICRC_AB_SPREAD", 1))));
+    k.skew = env("ICRC_AB_SKEW", -1);
+    k.skew_oct = env("ICRC_AB_SKEW_OCT", -1);
+    k.skew_long = env("ICRC_AB_SKEW_LONG", -1);
+    k.split = static_cast<uint32_t>(std::max(0, env("ICRC_AB_SPLIT", 0)));
+    k.hybrid_seq = env("ICRC_AB_HYBRID_SEQ", 0);
+    k.long_grid_mult = std::max(1, env("ICRC_AB_LONG_GRID", 1));
+    k.long_cus = env("ICRC_AB_LONG_CUS", 0);
+#endif
+    return k;
+}
+
 // Launch a batch.  A variant forced on the engine runs alone.  A batch of at most one packet per
 // wave runs on the one-packet pipeline alone.  Otherwise: a uniform strided
 // batch runs on the one-packet pipeline (kDefaultVariant) when its packets are long, on the oct
@@ -136,22 +166,16 @@ int grid_for(const icrc_engine *e, uint32_t n);
 // long-packet workgroups take each CU as the oct ones retire; under a forced hybrid variant (A/B)
 // two kernels on the caller's stream and the engine's side stream, forked and joined by events.
 int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
+    const DispatchKnobs k = dispatch_knobs();
     // spread (small host-mapped batches): one workgroup per packet up to #CUs, so that as many CUs
     // as possible read host memory over PCIe at once
-    uint32_t spread_per_wg = 1;  // packets per workgroup of a spread launch
-#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_SPREAD = packets per workgroup of a spread (small host-mapped) launch
-    if (const char *v = std::getenv("ICRC_AB_SPREAD")) spread_per_wg = std::max(1, std::min(16, std::atoi(v)));
-#endif
-    const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>((p.n + spread_per_wg - 1) / spread_per_wg, 1u),
+    const int grid = p.spread ? static_cast<int>(std::min<uint32_t>(std::max<uint32_t>((p.n + k.spread_per_wg - 1) / k.spread_per_wg, 1u),
                                                                     static_cast<uint32_t>(e->num_cu)))
                               : grid_for(e, p.n);
     p.split_len = 0;
-#ifdef ICRC_AB_BUILD  // A/B: the persistent waves' work skew (BatchParams::skew), read per call:
-    // ICRC_AB_SKEW both kernels, ICRC_AB_SKEW_OCT / ICRC_AB_SKEW_LONG one of them
-    if (const char *v = std::getenv("ICRC_AB_SKEW")) p.skew = static_cast<uint32_t>(std::atoi(v)) * 0x10001u;
-    if (const char *v = std::getenv("ICRC_AB_SKEW_OCT")) p.skew = (p.skew & 0xFFFF0000u) | (std::atoi(v) & 0xFFFF);
-    if (const char *v = std::getenv("ICRC_AB_SKEW_LONG")) p.skew = (p.skew & 0xFFFFu) | (static_cast<uint32_t>(std::atoi(v)) << 16);
-#endif
+    if (k.skew >= 0) p.skew = static_cast<uint32_t>(k.skew) * 0x10001u;
+    if (k.skew_oct >= 0) p.skew = (p.skew & 0xFFFF0000u) | (static_cast<uint32_t>(k.skew_oct) & 0xFFFFu);
+    if (k.skew_long >= 0) p.skew = (p.skew & 0xFFFFu) | (static_cast<uint32_t>(k.skew_long) << 16);
     if (e->variant >= 0 && e->variant < icrc::kHybridVariantBase) {
         p.variant = e->variant;
         return icrc::launch_batch(mode, p, grid, stream);
@@ -174,39 +198,18 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
         return icrc::launch_batch(mode, p, grid, stream);
     }
     p.variant = short_variant;
-    p.split_len = split;
-#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_SPLIT = the length split of ragged batches (oct takes L < split)
-    if (const char *v = std::getenv("ICRC_AB_SPLIT")) p.split_len = std::min<uint32_t>(split, static_cast<uint32_t>(std::atoi(v)));
-#endif
+    p.split_len = k.split ? std::min(split, k.split) : split;
     // Default: both halves in one launch (the fused hybrid kernel).  A forced hybrid variant
     // (100 + q, 200 + q: A/B) keeps the two-stream fork / join below.
     if (!hybrid_forced) {
-#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_HYBRID_SEQ = 1: the two halves as two kernels one after the other on the
-        // caller's stream (oct, then long-packet); 2: long-packet first
-        if (const char *v = std::getenv("ICRC_AB_HYBRID_SEQ")) {
-            const int seq = std::atoi(v);
-            if (seq == 1 || seq == 2) {
-                int rc = seq == 1 ? icrc::launch_batch(mode, p, grid, stream) : icrc::launch_long(mode, p, grid, stream);
-                if (rc == ICRC_OK) rc = seq == 1 ? icrc::launch_long(mode, p, grid, stream) : icrc::launch_batch(mode, p, grid, stream);
-                return rc;
-            }
+        if (k.hybrid_seq == 1 || k.hybrid_seq == 2) {
+            const bool oct_first = k.hybrid_seq == 1;
+            int rc = oct_first ? icrc::launch_batch(mode, p, grid, stream) : icrc::launch_long(mode, p, grid, stream);
+            if (rc == ICRC_OK) rc = oct_first ? icrc::launch_long(mode, p, grid, stream) : icrc::launch_batch(mode, p, grid, stream);
+            return rc;
         }
-#endif
-        int grid_long = grid;
-#ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_LONG_GRID = long-packet workgroups per oct workgroup
-        static const int long_mult = [] {
-            const char *v = std::getenv("ICRC_AB_LONG_GRID");
-            return v ? std::max(1, std::atoi(v)) : 1;
-        }();
-        grid_long = grid * long_mult;
-        // ICRC_AB_LONG_CUS = k: k CUs run long-packet workgroups from the start (grid - k oct
-        // workgroups, k long ones), instead of the long half waiting for oct workgroups to retire
-        if (const char *v = std::getenv("ICRC_AB_LONG_CUS")) {
-            const int k = std::atoi(v);
-            if (k > 0 && k < grid) return icrc::launch_hybrid(mode, p, grid - k, k, stream);
-        }
-#endif
-        return icrc::launch_hybrid(mode, p, grid, grid_long, stream);
+        if (k.long_cus > 0 && k.long_cus < grid) return icrc::launch_hybrid(mode, p, grid - k.long_cus, k.long_cus, stream);
+        return icrc::launch_hybrid(mode, p, grid, grid * k.long_grid_mult, stream);
     }
     std::lock_guard<std::mutex> g(e->fork_mu);
     HIP_TRY(hipEventRecord(e->fork_ev, static_cast<hipStream_t>(stream)));
