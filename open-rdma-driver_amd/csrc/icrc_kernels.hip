@@ -465,8 +465,10 @@ __device__ __forceinline__ void send_record(SendResults &r, uint32_t *pkt_len, u
 }
 
 // D: packets whose payload rows are in flight while one is processed; LAUX / SAUX: cache policy of
-// the payload loads / wire stores (0 default, 2 nt).  The product runs <1, 0, 0>.
-template <int D, int LAUX = 0, int SAUX = 0>
+// the payload loads / wire stores (0 default, 2 nt).  The product runs <1, 0, 0>.  (A/B only:
+// CUT 1 folds the rows by XOR instead of the table steps and final products, CUT 2 also drops the
+// header / mask / pad selects: the copy the kernel does, with its loads, stores and ring.)
+template <int D, int LAUX = 0, int SAUX = 0, int CUT = 0>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const uint8_t *src, uint64_t src_bytes,
                                                                           const icrc_write_msg *msgs, uint32_t nmsgs,
                                                                           uint32_t npk, uint8_t *wire, uint64_t wire_bytes,
@@ -568,16 +570,17 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
         for (int j = 0; j < kRows; ++j) {
             const int pw = g.k0 - 1 + static_cast<int>(lane) + 64 * j;
             uint32_t w = u[j];
-            w = (j == jh && inA) ? hA : ((j == jh + 1 && inB) ? hB : w);
-            if (j == kRows - 1) {  // the packet's last word: payload bytes only, then the zero pad
+            if constexpr (CUT < 2) w = (j == jh && inA) ? hA : ((j == jh + 1 && inB) ? hB : w);
+            if (CUT < 2 && j == kRows - 1) {  // the packet's last word: payload bytes only, then the zero pad
                 const int keep = static_cast<int>(room) - 4 * pw;
                 w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
             __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, SAUX);
-            const uint32_t uu = w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u));
-            acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
+            const uint32_t uu = CUT < 2 ? w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u)) : w;
+            if constexpr (CUT == 0) acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
+            else acc ^= uu;
         }
-        const uint32_t crc = ~wave_xor(final_mul(lds, acc, c.fin));
+        const uint32_t crc = ~wave_xor(CUT == 0 ? final_mul(lds, acc, c.fin) : acc);
         const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
             pbase, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
@@ -951,13 +954,16 @@ int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
     if (p.npackets == 0) return ICRC_OK;
     if (grid < 1) grid = 1;
     hipStream_t s = static_cast<hipStream_t>(stream);
-#define ICRC_PK(D, LA, SA)                                                                                          \
-    hipLaunchKernelGGL((icrc_packetize_kernel<D, LA, SA>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p.src, p.src_bytes, \
+#define ICRC_PK(D, LA, SA, ...)                                                                                     \
+    hipLaunchKernelGGL((icrc_packetize_kernel<D, LA, SA, ##__VA_ARGS__>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p.src, p.src_bytes, \
                        p.msgs, p.nmsgs, p.npackets, p.wire, p.wire_bytes, p.pkt_len, p.icrc, p.table)
 #ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK = 0 the product shape; 1: two packets in flight; 2: nt wire stores;
-    // 3: nt payload loads; 4: nt loads and stores
+    // 3: nt payload loads; 4: nt loads and stores; 5: rows XOR-folded (no CRC tables); 6: 5 without
+    // the header / mask / pad selects (results wrong by design for 5 and 6)
     const char *v = std::getenv("ICRC_AB_PK");
     switch (v ? std::atoi(v) : 0) {
+    case 5: ICRC_PK(1, 0, 0, 1); break;
+    case 6: ICRC_PK(1, 0, 0, 2); break;
     case 1: ICRC_PK(2, 0, 0); break;
     case 2: ICRC_PK(1, 0, 2); break;
     case 3: ICRC_PK(1, 2, 0); break;

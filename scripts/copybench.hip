@@ -123,6 +123,16 @@ __global__ __launch_bounds__(1024) void read_rows(const uint8_t *src, uint32_t *
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// COPY_RAND=1: the source filled with splitmix64 bytes instead of a constant
+__global__ void fill_rand(uint64_t *p, size_t n8) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
 __global__ void flat_x4(const uint4 *s, uint4 *d, size_t n16) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) d[i] = s[i];
 }
@@ -152,6 +162,12 @@ int main() {
     CK(hipMalloc(&src, src_bytes));
     CK(hipMalloc(&dst, (size_t)kN * kWire + 4096));
     CK(hipMemset(src, 0x5a, src_bytes));
+    const bool rnd = getenv("COPY_RAND") && atoi(getenv("COPY_RAND")) == 1;
+    if (rnd) {
+        fill_rand<<<cus * 4, 256>>>((uint64_t *)src, src_bytes / 8);
+        CK(hipDeviceSynchronize());
+    }
+    fprintf(stderr, "source: %s\n", rnd ? "splitmix64 bytes" : "constant 0x5a");
     CK(hipMemset(dst, 0, (size_t)kN * kWire));
     const int reps = 10;
     const double wire_bytes = (double)kN * (kPay + kPay);  // payload read + payload written

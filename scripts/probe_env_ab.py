@@ -30,14 +30,18 @@ def main():
            "C2nr": dict(ragged_frac=0.0)}
     jobs = {}
     for name in os.environ.get("JOBS", "C2,C2m").split(","):
-        if name == "PK":  # the fused send packetizer: 192 x 16 MiB WRITE -> 786 K x 4156-B packets
+        if name in ("PK", "PKc"):  # the fused send packetizer: 192 x 16 MiB WRITE -> 786 K x 4156-B packets
+            # (PKc: the payload one constant byte instead of random bytes)
             MSG, SLOT = 16 << 20, 28 + 28 + 4096 + 4
             specs = [dict(local_va=0x7F0000000000 + i * MSG, remote_va=0x7E0000000000 + i * MSG, payload_offset=i * MSG,
                           total_len=MSG, pmtu=4096, rkey=0x2000003, dqpn=2 + i, psn=0, msn=i & 0xFFFF,
                           dst_ip=0xC0A80003, kind=0) for i in range(192)]
             msgs = icrc_amd.write_messages(specs, slot_stride=SLOT)
             npk = int(msgs["npackets"].sum())
-            d_src = torch.randint(0, 256, (192 * MSG,), dtype=torch.uint8, device="cuda")
+            if name == "PKc":
+                d_src = torch.full((192 * MSG,), 0x5A, dtype=torch.uint8, device="cuda")
+            else:
+                d_src = torch.randint(0, 256, (192 * MSG,), dtype=torch.uint8, device="cuda")
             d_wire = torch.empty(npk * SLOT, dtype=torch.uint8, device="cuda")
             d_msgs = dev(msgs.view(np.uint8))
             d_len = torch.zeros(npk, dtype=torch.int32, device="cuda")
@@ -79,7 +83,8 @@ def main():
                 times[(j, v)].append(e0.elapsed_time(e1) / 10)
                 got = out.cpu().numpy().copy()
                 ref.setdefault(j, got)
-                assert np.array_equal(ref[j], got), (j, v)
+                if os.environ.get("AB_CHECK", "1") == "1":  # 0 for ablations (wrong results by design)
+                    assert np.array_equal(ref[j], got), (j, v)
     for (j, v), ts in times.items():
         nb = jobs[j][1]
         med = float(np.median(ts))
