@@ -76,6 +76,9 @@ def parse(argv=None):
     ap.add_argument("--launch-timeout", type=float, default=540.0,
                     help="seconds: the launcher kills the whole rank group and exits 3 when the ranks have not "
                          "finished by then (N > 1)")
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="initialise the RCCL process group (barriers, all-reduce, all-gather) even at world "
+                         "size 1: rehearses the N > 1 path on a one-GPU box (run under torch.distributed.run)")
     ap.add_argument("--cpu-stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--inject-fault-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
@@ -162,7 +165,7 @@ def time_steps(fn, steps: int, warmup: int, world: int, sync, barrier):
     for _ in range(warmup):
         fn()
     sync()
-    if world > 1:
+    if barrier is not None:
         barrier()
     sync()
     ev = None
@@ -178,7 +181,7 @@ def time_steps(fn, steps: int, warmup: int, world: int, sync, barrier):
     if ev:
         ev[1].record()
     sync()
-    if world > 1:
+    if barrier is not None:
         barrier()
     sync()
     wall = time.perf_counter() - t0
@@ -190,7 +193,7 @@ def time_kernel(fn, steps: int, warmup: int, world: int):
     import torch
     import torch.distributed as dist
 
-    return time_steps(fn, steps, warmup, world, torch.cuda.synchronize, dist.barrier)
+    return time_steps(fn, steps, warmup, world, torch.cuda.synchronize, dist.barrier if dist.is_initialized() else None)
 
 
 ARGS = None
@@ -226,7 +229,9 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
             f"({torch.cuda.device_count()} visible)")
         return 2
     torch.cuda.set_device(local)
-    if world > 1:
+    if args.dist_rehearsal and "MASTER_ADDR" not in os.environ:  # not under torch.distributed.run
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    if world > 1 or args.dist_rehearsal:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=_dist_timeout(args))
     import icrc_amd
     from icrc_amd import shard, workloads
@@ -340,7 +345,7 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
 
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     if agg.failures:
