@@ -99,7 +99,7 @@ void *icrc_engine_stream(const icrc_engine *engine);
  *        compacting long-packet walker);
  *   301 / 302  the receive parse as one fused pass on any batch (S = 2 / S = 1).
  * Other values: ICRC_EINVAL.  The quad kernels (20, 24-26, 120-126, 220-226) and the diagnostics
- * whose results are wrong by design (15, 18, 19, 21, 22, 31, 32, 35, 41-53, 141-153, 241-253)
+ * whose results are wrong by design (15, 18, 19, 21-23, 31, 32, 35, 41-53, 141-153, 241-253)
  * exist only in the A/B library libicrc_amd_ab.so (built with ICRC_AB_BUILD), which no product
  * path loads. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);

@@ -826,6 +826,7 @@ using RingLoadsOnly = RingAblation<kStreamAux, kCutLoadsOnly>;
 using RingCrcOnly = RingAblation<kStreamAux, kCutCrcOnly>;
 using RingNoFinal = RingAblation<kStreamAux, kCutNoFinal>;
 using RingNoStore = RingAblation<kStreamAux, kCutNoStore>;
+using RingBare = RingAblation<kStreamAux, kCutBare>;
 #endif
 template <int MODE>
 static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
@@ -840,6 +841,7 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 19: ICRC_LAUNCH(2, 1, RingLoadsOnly, false); break;  // loads only of 16's ring
     case 21: ICRC_LAUNCH(2, 1, RingNoFinal, false); break;   // 16 without final products
     case 22: ICRC_LAUNCH(2, 1, RingNoStore, false); break;   // 16 without result stores
+    case 23: ICRC_LAUNCH(2, 1, RingBare, false); break;      // 19 without final products and stores
     case 20:
     case 24:
     case 25:

@@ -107,14 +107,15 @@ struct Ring {
 };
 #ifdef ICRC_AB_BUILD
 // LOADS_ONLY: variants 15, 19 (the loads-only denominator bench.py reports); CRC_ONLY: 18;
-// NO_FINAL: 21; NO_STORE: 22 (the result stores of every block but the chunk's last).
-enum RingCut { kCutLoadsOnly, kCutCrcOnly, kCutNoFinal, kCutNoStore };
+// NO_FINAL: 21; NO_STORE: 22 (the result stores of every block but the chunk's last); BARE: 23
+// (loads only, without the final products and the per-block stores: the bare read walk).
+enum RingCut { kCutLoadsOnly, kCutCrcOnly, kCutNoFinal, kCutNoStore, kCutBare };
 template <int AUX, int CUT>
 struct RingAblation : Ring<AUX> {
     static constexpr bool kLoads = CUT != kCutCrcOnly;
-    static constexpr bool kSteps = CUT != kCutLoadsOnly;
-    static constexpr bool kFinal = CUT != kCutNoFinal;
-    static constexpr bool kStores = CUT != kCutNoStore;
+    static constexpr bool kSteps = CUT != kCutLoadsOnly && CUT != kCutBare;
+    static constexpr bool kFinal = CUT != kCutNoFinal && CUT != kCutBare;
+    static constexpr bool kStores = CUT != kCutNoStore && CUT != kCutBare;
 };
 #endif
 

@@ -2,7 +2,7 @@
 """A/B the ICRC kernel variants in ONE process, interleaved rounds (methodology rule 24):
 C1 (1 Mi x 4156 B, strided) and C2 (mixed MTU, ragged) for each variant; checks that every
 variant returns identical ICRCs.  Prints one JSON line per (workload, variant)."""
-DIAGNOSTIC = {15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 50, 53}  # ablations (loads-only / CRC-only / no loads): wrong results by design
+DIAGNOSTIC = {15, 18, 19, 21, 22, 23, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 50, 53}  # ablations (loads-only / CRC-only / no loads): wrong results by design
 import json
 import os
 import sys

@@ -51,8 +51,8 @@ def main():
                                         d_wire.numel(), d_len.data_ptr(), d_icrc.data_ptr(), s),
                           npk * (4096 + 4156 + 8), d_icrc, (d_src, d_wire, d_msgs, d_len))
             continue
-        if name == "S316":
-            w = workloads.write_middle_stream(1 << 22, pmtu=256)
+        if name in ("S316", "C1"):
+            w = workloads.write_middle_stream(1 << 22, pmtu=256) if name == "S316" else workloads.write_middle_stream(1 << 20)
             L = int(w.lens[0])
             b = workloads.synthesize(eng, w, stream=s)
             out = torch.zeros(w.n, dtype=torch.int32, device="cuda")
