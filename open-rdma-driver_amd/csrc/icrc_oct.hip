@@ -704,6 +704,31 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_kernel(BatchPara
     if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, OctProduct>(p, lds4, blockIdx.x, g_oct);
     else long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
 }
+#ifdef ICRC_AB_BUILD
+// A/B (ICRC_AB_HYBRID_STAMP=1, compute): the hybrid kernel with each workgroup's start and end
+// (s_memrealtime, 100 MHz) and kind stored in g_hybrid_stamps, entry b = {start lo, start hi, end
+// lo, end hi, 0 = oct / 1 = long} of workgroup b, read back by icrc_ab_hybrid_stamps: when the
+// long-packet workgroups start and end against the oct ones' ends (scripts/probe_hybrid_timeline.py).
+constexpr uint32_t kStampGroups = 8192;
+__device__ uint32_t g_hybrid_stamps[5 * kStampGroups];
+template <bool COMPACT>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_stamp_kernel(BatchParams p, uint32_t g_oct) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < g_oct) oct_body<kCompute, true, false, OctProduct>(p, lds4, blockIdx.x, g_oct);
+    else long_body<kCompute, COMPACT, false>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < kStampGroups) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        uint32_t *e = g_hybrid_stamps + 5u * blockIdx.x;
+        e[0] = static_cast<uint32_t>(t0);
+        e[1] = static_cast<uint32_t>(t0 >> 32);
+        e[2] = static_cast<uint32_t>(t1);
+        e[3] = static_cast<uint32_t>(t1 >> 32);
+        e[4] = blockIdx.x < g_oct ? 0u : 1u;
+    }
+}
+#endif
 
 }  // namespace
 
@@ -778,6 +803,14 @@ int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, v
             else ICRC_H(M, false, false);             \
         }                                             \
     } while (0)
+#ifdef ICRC_AB_BUILD
+    const char *st = std::getenv("ICRC_AB_HYBRID_STAMP");
+    if (st && std::atoi(st) == 1 && mode == kCompute && !p.trailer) {
+        if (p.long_variant == 1) hipLaunchKernelGGL((icrc_hybrid_stamp_kernel<true>), g, dim3(kThreadsPerGroup), 0, s, p, go);
+        else hipLaunchKernelGGL((icrc_hybrid_stamp_kernel<false>), g, dim3(kThreadsPerGroup), 0, s, p, go);
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
+#endif
     if (mode == kCompute) ICRC_HM(kCompute);
     else ICRC_HM(kVerify);
 #undef ICRC_HM
@@ -786,3 +819,12 @@ int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, v
 }
 
 }  // namespace icrc
+
+#ifdef ICRC_AB_BUILD
+// A/B library only (not in include/icrc.h): copy the last stamp launch's n_groups x 5 words.
+extern "C" int icrc_ab_hybrid_stamps(uint32_t *dst, uint32_t n_groups) {
+    if (n_groups > icrc::kStampGroups) n_groups = icrc::kStampGroups;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(icrc::g_hybrid_stamps), 5u * n_groups * sizeof(uint32_t), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
