@@ -27,6 +27,10 @@ achieved GB/s (HIP events on the launch stream) vs the 8.0 TB/s HBM3E peak.  cpu
 the CPU port of compute_icrc with a crc32fast-equivalent PCLMULQDQ core (oracle/icrc_fast.c),
 rank 0 / N=1 only, on a bounded sample of the same packets.
 
+Every GPU measurement repeats its step untimed for --settle-ms (150) before its W warm-up steps:
+the first ~30 launches in a fresh process run slower while the clocks settle (rocprof trace of
+the plain bench: 0.67 -> 0.76 -> 0.677 ms over launches 1-25).
+
 --cpu-stub (tests only): the same launcher, rank handling, barriers and aggregation on gloo
 with a CPU stand-in step (zlib.crc32 of every packet, not the ICRC and not the product), so
 the N>1 plumbing is exercised on a machine without GPUs (tests/test_multi_rank.py).
@@ -60,6 +64,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="before the W warm-up steps of every GPU measurement, repeat the step for this "
+                         "long (untimed): a fresh process's first ~30 launches of the C1 kernel run up "
+                         "to 12 %% slower while the GPU's clocks settle (profiles/r04_clock_settle/)")
     ap.add_argument("--packets", type=int, default=1 << 20,
                     help="packets per GPU (weak scaling) or in total (strong scaling)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
@@ -162,6 +170,14 @@ def _dist_timeout(args):
 def time_steps(fn, steps: int, warmup: int, world: int, sync, barrier):
     """Warmup, barrier + sync, K timed steps, sync + barrier.  Returns (this rank's wall seconds,
     kernel ms per step from HIP events on the launch stream or None)."""
+    if ARGS is not None and not ARGS.cpu_stub and ARGS.settle_ms > 0:
+        # untimed: launches in bursts of 4 until settle_ms of wall time, so the timed steps see the
+        # steady clocks and not the power-management transient of the first launches
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < ARGS.settle_ms:
+            for _ in range(4):
+                fn()
+            sync()
     for _ in range(warmup):
         fn()
     sync()
