@@ -651,6 +651,15 @@ def fused_send_receive(eng, stream, args, world):
                              "lengths_ok": lens_ok}
     if not lens_ok:
         return out
+    # same-box denominator: a device-to-device copy of the payload bytes (hipMemcpyAsync through
+    # torch) into the wire buffer, then the packets are rebuilt for the receive leg
+    _, cms = time_kernel(lambda: d_wire[:src_bytes].copy_(d_src), args.steps, args.warmup, world)
+    send()
+    torch.cuda.synchronize()
+    out["packetize_send"]["copy_reference"] = {
+        "what": "d2d copy of the same payload bytes (hipMemcpyAsync), same box, timed like the kernel",
+        "ms": round(cms, 4), "hbm_GB/s": round(2 * src_bytes / (cms * 1e-3) / 1e9, 1),
+        "packetize_rate_vs_copy_rate": round((alg / kms) / (2 * src_bytes / cms), 4)}
     del d_src
     d_off = torch.arange(npk, dtype=torch.int64, device="cuda") * (28 + 28 + pmtu + 4)
     d_desc = torch.empty(npk * icrc_amd.RX_DESC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
