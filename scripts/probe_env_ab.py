@@ -59,7 +59,10 @@ def main():
             jobs[name] = (lambda b=b, out=out, n=w.n, L=L: eng.compute_strided(b.data_ptr(), L, L, n, out.data_ptr(),
                                                                                False, s), w.n * L, out, b)
             continue
-        w = workloads.mixed_mtu_stream(4 << 20, **kws[name])
+        if name == "R4K":  # 1 Mi x 4156-B packets as a ragged batch (offset / length arrays): every packet long
+            w = workloads.write_middle_stream(1 << 20)
+        else:
+            w = workloads.mixed_mtu_stream(4 << 20, **kws[name])
         b = workloads.synthesize(eng, w, stream=s)
         o, l = dev(w.off), dev(w.lens)
         out = torch.zeros(w.n, dtype=torch.int32, device="cuda")
