@@ -51,6 +51,25 @@ __device__ __forceinline__ void meta_fetch(const BatchParams &p, MetaBlock &mb, 
     mb.block = block;
 }
 
+// the packet at byte offset `off` of length L into slot m (kind 1 regular / 2 irregular; LONG:
+// kind 0 for the short-packet kernel's packets)
+template <int MODE, bool LONG>
+__device__ __forceinline__ void slot_classify(const BatchParams &p, uint64_t off, uint32_t L, SlotMeta &m) {
+    if (LONG && L < p.split_len) return;
+    m.pkt = p.base + off;
+    m.L = L;
+    m.kind = 2;
+    if (L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(m.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+        const int N = static_cast<int>(stream_words<MODE>(L));
+        const int R = (N + 63) >> 6;
+        if (R <= kRows) {
+            m.kind = 1;
+            m.R = R;
+            m.k0 = N - 64 * R;
+        }
+    }
+}
+
 // LONG: the long-packet half of a split batch — packets with L < p.split_len belong to the short-
 // packet kernel and leave the slot empty (kind 0: no loads, no result).
 template <int MODE, bool LONG = false>
@@ -74,19 +93,7 @@ __device__ __forceinline__ void slot_meta(const BatchParams &p, MetaBlock &mb, b
         off = static_cast<uint64_t>(lo + q) * p.stride;
         L = p.ulen;
     }
-    if (LONG && L < p.split_len) return;
-    m.pkt = p.base + off;
-    m.L = L;
-    m.kind = 2;
-    if (L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(m.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
-        const int N = static_cast<int>(stream_words<MODE>(L));
-        const int R = (N + 63) >> 6;
-        if (R <= kRows) {
-            m.kind = 1;
-            m.R = R;
-            m.k0 = N - 64 * R;
-        }
-    }
+    slot_classify<MODE, LONG>(p, off, L, m);
 }
 
 // Loads of one packet's rows; rows past the
@@ -104,8 +111,19 @@ struct Ring {
     static constexpr bool kSteps = true;   // the row steps (else the rows XOR-folded: a memory-pipeline bound)
     static constexpr bool kFinal = true;   // the per-lane final products M^(64 - l)
     static constexpr bool kStores = true;  // the result stores of every block
+    // ragged batches on the long-packet half's dense walk: each packet's (offset, length) by scalar
+    // loads one set ahead of its row loads (run_pipelined SM; the vector blocks are a conditional
+    // vector load inside the ring: 4.8 % slower on 1 Mi x 4156 B ragged,
+    // profiles/r04_ab_ragged_scalar_meta.jsonl).  The batch kernel keeps the vector blocks: its
+    // small batches (a wave per packet) wait longer for a scalar load.
+    static constexpr bool kScalarMeta = true;
 };
 #ifdef ICRC_AB_BUILD
+// (A/B, variant 27) the default ring with the (offset, length) of ragged batches in 64-packet
+// vector blocks (the ring before round 4's scalar loads)
+struct RingVectorMeta : Ring<kStreamAux> {
+    static constexpr bool kScalarMeta = false;
+};
 // LOADS_ONLY: variants 15, 19 (the loads-only denominator bench.py reports); CRC_ONLY: 18;
 // NO_FINAL: 21; NO_STORE: 22 (the result stores of every block but the chunk's last); BARE: 23
 // (loads only, without the final products and the per-block stores: the bare read walk).
@@ -548,7 +566,11 @@ __device__ __forceinline__ void process_set(const BatchParams &p, const char *ld
 // it waits for the table share, so that the three memory latencies overlap (a small batch, one
 // packet per wave, is made of little else); then every wave, with or without packets, writes its
 // share to LDS and joins the barrier.
-template <int MODE, int S, int D, class A, int PARSE = 0, bool LONG = false, bool TRAILER = false, bool TABLE = false>
+// SM: a ragged batch's (offset, length) by scalar loads one set ahead of the row loads (the long-
+// packet half's dense walk, whose waves hold hundreds of packets) instead of 64-packet vector
+// blocks read back lane by lane.
+template <int MODE, int S, int D, class A, int PARSE = 0, bool LONG = false, bool TRAILER = false, bool TABLE = false,
+          bool SM = false>
 __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *lds, const LaneConsts &c,
                                               uint32_t lane, uint32_t lo, uint32_t nq, TableShare *tv = nullptr) {
     constexpr int B = D + 1;
@@ -568,8 +590,36 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
+    // (A::kScalarMeta, ragged batches) the (offset, length) of one set's slots by scalar loads,
+    // issued one set before its row loads need them
+    const bool smeta = SM && ragged;
+    uint64_t nm_off[S];
+    uint32_t nm_len[S];
+    auto smeta_load = [&](uint32_t set) __attribute__((always_inline)) {
+        typedef __attribute__((address_space(4))) const uint64_t c_u64;
+        typedef __attribute__((address_space(4))) const uint32_t c_u32;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const uint32_t q = set * S + static_cast<uint32_t>(s);
+            const uint32_t i = lo + q;
+            nm_off[s] = 0;
+            nm_len[s] = 0;
+            if (q < nq) {  // uniform: past the range nothing is read
+                nm_off[s] = p.off ? ((c_u64 *)p.off)[i] : static_cast<uint64_t>(i) * p.stride;
+                nm_len[s] = p.len ? ((c_u32 *)p.len)[i] : p.ulen;
+            }
+        }
+    };
+    auto smeta_slot = [&](uint32_t set, int s, SlotMeta &sm) __attribute__((always_inline)) {
+        sm.kind = 0;
+        sm.R = 0;
+        sm.k0 = 0;
+        sm.pkt = p.base;
+        sm.L = 0;
+        if (set * S + static_cast<uint32_t>(s) < nq) slot_classify<MODE, LONG>(p, nm_off[s], nm_len[s], sm);
+    };
     if constexpr (TABLE) {
-        if (ragged && nq != 0) meta_fetch(p, mb, lo, lo + nq, 0, lane);
+        if (ragged && nq != 0 && !smeta) meta_fetch(p, mb, lo, lo + nq, 0, lane);
         table_fetch(*tv, p.table);
     }
 #pragma unroll
@@ -577,13 +627,16 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
         // TABLE: unconditional (an empty slot's loads are out of range), so that the wait for the
         // table share below counts exactly these loads behind it
         if (TABLE || static_cast<uint32_t>(d) < nsets) {
+            if (smeta) smeta_load(static_cast<uint32_t>(d));
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta<MODE, LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
+                if (smeta) smeta_slot(static_cast<uint32_t>(d), s, m[d][s]);
+                else slot_meta<MODE, LONG>(p, mb, ragged, lo, d * S + s, nq, lane, m[d][s]);
                 slot_load<A, MODE, TRAILER>(m[d][s], lane, u[d][s]);
             }
         }
     }
+    if (smeta) smeta_load(static_cast<uint32_t>(D));
     if constexpr (TABLE) {
         table_store(*tv, const_cast<uint4 *>(reinterpret_cast<const uint4 *>(lds)));
         if (nq == 0) return;
@@ -601,9 +654,11 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
             if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int s = 0; s < S; ++s) {
-                slot_meta<MODE, LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
+                if (smeta) smeta_slot(tp, s, m[bp][s]);
+                else slot_meta<MODE, LONG>(p, mb, ragged, lo, tp * S + s, nq, lane, m[bp][s]);
                 slot_load<A, MODE, TRAILER>(m[bp][s], lane, u[bp][s]);
             }
+            if (smeta) smeta_load(tp + 1u);
             if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(0);
             const uint32_t q0 = ts * S;
             process_set<MODE, S, A, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], q0, rb, hm, ra, lo);
@@ -753,7 +808,7 @@ __device__ __forceinline__ bool wg_any_split(const BatchParams &p, uint4 *lds4, 
 
 // The long-packet kernel's work for workgroup `bid` of `nblk` (its own kernel, or the long-packet
 // workgroups of the fused hybrid kernel, icrc_oct.hip).
-template <int MODE, bool COMPACT, bool TRAILER>
+template <int MODE, bool COMPACT, bool TRAILER, class LA = Ring<kStreamAux>>
 __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
     if (p.split_len != 0 && p.len != nullptr) {
         // A workgroup whose packets are all the oct kernel's exits before its 160 KiB table load.
@@ -770,10 +825,20 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     c.fin = kFinalBase + lane * 4u;
     const uint32_t tw = nblk * kWavesPerGroup;
     const uint32_t chunk = wave_chunk(p.n, tw);
+    const uint64_t g0 = static_cast<uint64_t>(bid) * kWavesPerGroup * chunk;
+    // The waves' shares: skewed by age as in the batch kernel (p.skew's long half) when the
+    // workgroup's range is dense with long packets (its first 64, the same sample in every wave),
+    // equal otherwise — on sparse ranges (C2) a skew measured slower
+    // (profiles/r03_probe_skew_long.jsonl; dense: profiles/r04_ab_long_dense_skew.jsonl).
+    uint32_t skew = 0u;
+    if (!COMPACT && p.len != nullptr && g0 < p.n) {
+        const uint64_t i = g0 + lane;
+        const uint64_t dm = __ballot(i < p.n && p.len[i] >= p.split_len);
+        const uint32_t ns = p.n - g0 < 64u ? static_cast<uint32_t>(p.n - g0) : 64u;
+        if (4u * static_cast<uint32_t>(__builtin_popcountll(dm)) >= 3u * ns) skew = p.skew >> 16;
+    }
     uint64_t lo64, hi64;
-    // equal shares: in the hybrid launch these workgroups fill CUs as the oct ones retire, and a
-    // skew measured slower on C2 (profiles/r03_probe_skew_long.jsonl)
-    wave_range(static_cast<uint64_t>(bid) * kWavesPerGroup * chunk, chunk, wave, 0u, lo64, hi64);
+    wave_range(g0, chunk, wave, skew, lo64, hi64);
     if (lo64 >= p.n) return;
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
@@ -787,7 +852,7 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, Ring<kStreamAux>, 0, true, TRAILER>(p, lds, c, lane, lo, nq);
+            run_pipelined<MODE, 2, 1, LA, 0, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
         else
             run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER>(p, lds, c, lane, lo, nq);
     }

@@ -698,11 +698,11 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_kernel(BatchParams 
 // are dispatched in index order, so the long-packet ones take each CU as its oct workgroup
 // retires — the overlap the two-stream fork / join gave, without its cross-queue wait (~19 us per
 // call, profiles/r02_hybrid_fused.jsonl) or the second launch.
-template <int MODE, bool TRAILER, bool COMPACT>
+template <int MODE, bool TRAILER, bool COMPACT, class LA = Ring<kStreamAux>>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_kernel(BatchParams p, uint32_t g_oct) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, OctProduct>(p, lds4, blockIdx.x, g_oct);
-    else long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
+    else long_body<MODE, COMPACT, TRAILER, LA>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
 }
 #ifdef ICRC_AB_BUILD
 // A/B (ICRC_AB_HYBRID_STAMP=1, compute): the hybrid kernel with each workgroup's start and end
@@ -804,6 +804,12 @@ int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, v
         }                                             \
     } while (0)
 #ifdef ICRC_AB_BUILD
+    // ICRC_AB_LONG_VMETA=1: the long half's dense walk with vector (offset, length) blocks
+    const char *vm = std::getenv("ICRC_AB_LONG_VMETA");
+    if (vm && std::atoi(vm) == 1 && mode == kCompute && !p.trailer && p.long_variant != 1) {
+        hipLaunchKernelGGL((icrc_hybrid_kernel<kCompute, false, false, RingVectorMeta>), g, dim3(kThreadsPerGroup), 0, s, p, go);
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
     const char *st = std::getenv("ICRC_AB_HYBRID_STAMP");
     if (st && std::atoi(st) == 1 && mode == kCompute && !p.trailer) {
         if (p.long_variant == 1) hipLaunchKernelGGL((icrc_hybrid_stamp_kernel<true>), g, dim3(kThreadsPerGroup), 0, s, p, go);

@@ -28,7 +28,7 @@ def main():
     rounds = int(os.environ.get("ROUNDS", "5"))
     launches = int(os.environ.get("LAUNCHES", "10"))
     # the product library (or ICRC_AMD_LIB's build) unless a variant exists only in the A/B build
-    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26, 49, 51, 52) for v in variants if v >= 0)
+    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26, 27, 49, 51, 52) for v in variants if v >= 0)
     eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library() if ab_only else None)
     s = torch.cuda.current_stream().cuda_stream
     jobs = {}
@@ -85,6 +85,16 @@ def main():
             jobs[name] = (lambda b2=b2, o2=o2, l2=l2, out2=out2, n=int(sel.sum()): eng.compute_batch(
                 b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), n, out2.data_ptr(), False, 0, s),
                 int(len_s.astype(np.uint64).sum()), out2)
+            continue
+        if name == "R4K":  # C1's packets as a ragged batch (offset / length arrays)
+            w2 = workloads.write_middle_stream(1 << 20)
+            b2 = workloads.synthesize(eng, w2, stream=s)
+            o2, l2 = dev(w2.off), dev(w2.lens)
+            out2 = torch.zeros(w2.n, dtype=torch.int32, device="cuda")
+            keep += [b2, o2, l2, out2]
+            jobs[name] = (lambda b2=b2, o2=o2, l2=l2, out2=out2, n=w2.n: eng.compute_batch(
+                b2.data_ptr(), o2.data_ptr(), l2.data_ptr(), n, out2.data_ptr(), False, 0, s),
+                int(w2.lens.astype(np.uint64).sum()), out2)
             continue
         kw = {"C2": {}, "C2k": dict(classes=(1024,)), "C2s": dict(classes=(256,)), "C2nr": dict(ragged_frac=0.0),
               "C2m": dict(classes=(256, 1024)), "C2snr": dict(classes=(256,), ragged_frac=0.0)}[name]
