@@ -568,6 +568,18 @@ def extra_measurements(eng, stream, args, world):
                                     "frac_of_peak": frac(kms, n * L)}
     del d_buf, d_out
 
+    # C1's packets as a ragged batch (offset / length arrays, the default hybrid dispatch): what a
+    # driver's packet buffers hand over; the arrays' 12 bytes per packet are not counted
+    d_buf = workloads.synthesize(eng, w, stream=stream)
+    d_off, d_len = dev(w.off), dev(w.lens)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    _, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
+                                                   d_out.data_ptr(), False, 0, stream),
+                         args.steps, args.warmup, world)
+    ex["compute_c1_ragged"] = {"kernel_ms": round(kms, 4), "GiB/s": round(n * L / (kms * 1e-3) / GIB, 1),
+                               "frac_of_peak": frac(kms, n * L)}
+    del d_buf, d_out, d_off, d_len
+
     # mixed MTU
     wm = workloads.mixed_mtu_stream(4 << 20)
     d_buf = workloads.synthesize(eng, wm, stream=stream)
