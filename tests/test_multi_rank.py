@@ -215,3 +215,42 @@ def test_bench_launcher_refuses_without_gpu_count():
                        capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
     assert p.returncode == 2, p.stderr[-2000:]
     assert "torch.distributed.run" not in p.stderr
+
+
+def test_time_steps_settles_before_warmup(monkeypatch):
+    """bench.time_steps: untimed repetitions for --settle-ms before the W warm-up steps (GPU runs
+    only: the cpu stub skips it), then exactly K timed steps."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    calls = {"n": 0}
+
+    def step():
+        calls["n"] += 1
+
+    bench.ARGS = bench.parse(["--settle-ms", "30", "--steps", "5", "--warmup", "2"])
+    assert bench.ARGS.settle_ms == 30.0 and not bench.ARGS.dist_rehearsal
+    monkeypatch.setattr(bench.ARGS, "cpu_stub", True)  # no torch.cuda events on the CPU
+    bench.time_steps(step, 5, 2, 1, lambda: None, None)
+    assert calls["n"] == 7  # the stub skips the settle phase
+    monkeypatch.setattr(bench.ARGS, "cpu_stub", False)
+    calls["n"] = 0
+
+    class _Ev:  # stand-in for torch.cuda.Event (no GPU here)
+        def __init__(self, **kw):
+            pass
+
+        def record(self):
+            pass
+
+        def elapsed_time(self, other):
+            return 1.0
+
+    import torch
+
+    monkeypatch.setattr(torch.cuda, "Event", _Ev)
+    t0 = __import__("time").perf_counter()
+    wall, kms = bench.time_steps(step, 5, 2, 1, lambda: None, None)
+    assert __import__("time").perf_counter() - t0 >= 0.03
+    assert calls["n"] > 7 and (calls["n"] - 7) % 4 == 0  # settle bursts of 4, then 2 + 5
+    assert kms == 1.0 / 5
