@@ -37,6 +37,7 @@ if [ "${PRESORT:-0}" = 1 ]; then
   cat $OUT/presort.jsonl; tail -3 $OUT/presort.err; stop_if_fatal $rc probe_presort
 fi
 if [ "${MSGAB:-0}" = 1 ]; then  # the round-3 library (one launch in flight) vs this build, alternating
+  # (recorded in profiles/r04_msg_submitter_ab.jsonl; _build/old_r03 is gpurun-ignored since: un-ignore to rerun)
   for r in 1 2; do
     for b in old_r03 new; do
       d=open-rdma-driver_amd/_build; [ $b = old_r03 ] && d=open-rdma-driver_amd/_build/old_r03
