@@ -410,13 +410,17 @@ KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_inte
 
 
 def kernel_source_hash() -> str:
-    """sha256 (16 hex digits) over the C1 kernel's sources as shipped in this tree."""
+    """sha256 (16 hex digits) over the C1 kernel's sources as shipped in this tree, comments and
+    blank lines removed (a comment edit does not orphan a traffic record; any code edit does)."""
     import hashlib
+    import re
 
     h = hashlib.sha256()
     for name in KERNEL_SOURCES:
-        with open(os.path.join(ROOT, "open-rdma-driver_amd", "csrc", name), "rb") as f:
-            h.update(name.encode() + b"\0" + f.read())
+        with open(os.path.join(ROOT, "open-rdma-driver_amd", "csrc", name), "r", encoding="utf-8") as f:
+            text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+        code = [ln.split("//", 1)[0].rstrip() for ln in text.splitlines()]
+        h.update(name.encode() + b"\0" + "\n".join(ln for ln in code if ln).encode())
     return h.hexdigest()[:16]
 LOADS_ONLY_VARIANT = 19  # A/B library: icrc_batch_kernel<.., S = 2, D = 1, loads only>, the default ring without the CRC
 

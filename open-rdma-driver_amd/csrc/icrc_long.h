@@ -119,8 +119,8 @@ struct Ring {
     static constexpr bool kScalarMeta = true;
 };
 #ifdef ICRC_AB_BUILD
-// (A/B, variant 27) the default ring with the (offset, length) of ragged batches in 64-packet
-// vector blocks (the ring before round 4's scalar loads)
+// (A/B, ICRC_AB_LONG_VMETA=1: the hybrid's dense long walk) the default ring with the (offset,
+// length) of ragged batches in 64-packet vector blocks (the ring before round 4's scalar loads)
 struct RingVectorMeta : Ring<kStreamAux> {
     static constexpr bool kScalarMeta = false;
 };
@@ -590,8 +590,8 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
     if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][S];
     uint32_t u[B][S][ring_words<MODE>()];
-    // (A::kScalarMeta, ragged batches) the (offset, length) of one set's slots by scalar loads,
-    // issued one set before its row loads need them
+    // (SM, ragged batches) the (offset, length) of one set's slots by scalar loads, issued one
+    // set before its row loads need them
     const bool smeta = SM && ragged;
     uint64_t nm_off[S];
     uint32_t nm_len[S];
