@@ -966,6 +966,41 @@ def _offsets_beyond_2gib(engine, icrc_amd):
     torch.cuda.empty_cache()
 
 
+def test_ragged_dense_long_walk_across_4GiB(engine):
+    """The hybrid launch's dense long-packet walk (scalar (offset, length) loads one set ahead, the
+    waves' age skew) on 12 288 packets of 4156 B whose offsets cross 2^32: compute with trailers,
+    verify against the oracle, then verify with a flipped bit every 97 packets."""
+    rng = np.random.default_rng(4097)
+    n, L = 12288, 4156
+    base = (1 << 32) - 6 * 1024 * L  # a quarter of the packets below 4 GiB, the rest above
+    total = base + n * L + 64
+    d_buf = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    pk = rng.integers(0, 256, n * L, dtype=np.uint8)
+    d_buf[base: base + n * L] = torch.from_numpy(pk).cuda()
+    off = base + np.arange(n, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(n, L, np.uint32)
+    d_off, d_len = dev(off), dev(lens)
+    d_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    engine.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out.data_ptr(), True, 0,
+                         stream_handle())
+    torch.cuda.synchronize()
+    rel = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    want = oracle_icrcs(pk, rel, lens)
+    np.testing.assert_array_equal(d_out.cpu().numpy().view(np.uint32), want)
+    bad = np.arange(0, n, 97)
+    for i in bad:
+        d_buf[int(off[i]) + 100] ^= 0x01
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), False, 0,
+                        stream_handle())
+    torch.cuda.synchronize()
+    expect = np.ones(n, np.uint8)
+    expect[bad] = 0
+    np.testing.assert_array_equal(d_ok.cpu().numpy(), expect)
+    del d_buf
+    torch.cuda.empty_cache()
+
+
 def test_empty_batches_are_noops(engine):
     """n == 0 on every device entry point: OK, nothing written (the reference's loops simply do
     not run on an empty packet list)."""
