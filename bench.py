@@ -76,6 +76,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (the parity sample still runs)")
     ap.add_argument("--check-packets", type=int, default=2048,
                     help="per rank: packets at each end of the shard checked against the CPU restatement")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs[2] / configs[3] legs of the default line (N = 1)")
+    ap.add_argument("--c2-only", action="store_true",
+                    help="time only the configs[2] kernel and print its leg (rocprofv3 --pmc passes)")
     ap.add_argument("--extra", action="store_true",
                     help="also time verify, trailer stores, mixed-MTU, 16 MiB round trip, packetizer, receive "
                          "parse and the host-resident path")
@@ -257,6 +261,12 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         log(f"bench.py: rank {rank}: engine on device {eng.ordinal}, expected LOCAL_RANK {local}")
         return 2
     stream = torch.cuda.current_stream().cuda_stream
+    if args.c2_only:
+        import oracle as orc
+
+        leg, fails = config_c2(eng, stream, args, world, orc)
+        print(json.dumps({"configs": {"c2": leg}}), flush=True)
+        return 1 if fails else 0
 
     # ---- C1 workload: weak = one QP stream per rank; strong = a shard of one stream ----
     if args.scaling == "weak":
@@ -356,6 +366,15 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         host = d_buf[: min(n, 16384) * L].cpu().numpy()
         result["cpu_baseline"], result["cpu_context"] = cpu_baseline(orc, host, L, d_out, args)
 
+    cfg_fails = 0
+    if world == 1 and not args.no_configs:  # configs[2] and [3] after the headline (value untouched)
+        del d_buf, d_out
+        torch.cuda.empty_cache()
+        c2, f2 = config_c2(eng, stream, args, world, orc)
+        c3, f3 = config_c3(eng, stream, args, world, orc)
+        result["configs"] = {"c2": c2, "c3": c3}
+        cfg_fails = f2 + f3
+
     if args.extra:
         result["extra"] = extra_measurements(eng, stream, args, world)
 
@@ -364,10 +383,85 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
-    if agg.failures:
-        log(f"bench.py: {agg.failures} ICRC mismatches against the CPU restatement")
+    if agg.failures or cfg_fails:
+        log(f"bench.py: {agg.failures + cfg_fails} ICRC mismatches against the CPU restatement")
         return 1
     return 0
+
+
+def config_c2(eng, stream, args, world, orc):
+    """configs[2] in the default line: the mixed-MTU batch (4 Mi packets, 256 B / 1 KiB / 4 KiB
+    payload classes, P ~ k^-1.5, 10 % ragged LAST packets; 1.82 GB) through the default ragged
+    dispatch (one hybrid launch), timed like the headline (settle, warm-up, HIP events on the launch
+    stream).  Its traffic ratio comes from the committed PMC record of this build's oct / long-packet
+    sources (PMC_C2_FILE), or is null.  Parity: 4096 packets (both ends of the batch) against the
+    CPU restatement.  Returns (leg, mismatches)."""
+    import torch
+
+    from icrc_amd import workloads
+
+    wm = workloads.mixed_mtu_stream(4 << 20)
+    d_buf = workloads.synthesize(eng, wm, stream=stream)
+    d_off, d_len = dev(wm.off), dev(wm.lens)
+    d_out = torch.zeros(wm.n, dtype=torch.int32, device="cuda")
+    _, kms = time_kernel(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n,
+                                                   d_out.data_ptr(), False, 0, stream),
+                         min(args.steps, 20), min(args.warmup, 5), world)
+    tot = int(wm.lens.astype(np.uint64).sum())
+    got = d_out.cpu().numpy().view(np.uint32)
+    fails = 0
+    for a, b in ((0, 2048), (wm.n - 2048, wm.n)):
+        lo, hi = int(wm.off[a]), int(wm.off[b - 1]) + int(wm.lens[b - 1])
+        host = d_buf[lo:hi].cpu().numpy()
+        want = orc.compute_icrc_batch(host, (wm.off[a:b] - np.uint64(lo)).astype(np.uint64), wm.lens[a:b])
+        fails += int(np.count_nonzero(got[a:b] != want))
+    leg = {"workload": "configs[2]: 4 Mi mixed-MTU packets (256 B / 1 KiB / 4 KiB classes, power-law, 10 % ragged), "
+                       "ragged (offset, length) arrays, one hybrid launch",
+           "packets": wm.n, "bytes": tot, "kernel_ms": round(kms, 4),
+           "GiB/s": round(tot / (kms * 1e-3) / GIB, 1),
+           "frac": round(tot / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic_ratio": None, "parity_checked": 4096, "parity_failures": fails}
+    tr = pmc_record(PMC_C2_FILE, C2_SOURCES, wm.n, None)
+    if tr is not None:
+        leg["traffic_ratio"] = tr["ratio_to_algorithmic"]
+        leg["traffic_source"] = f"profiles/{PMC_C2_FILE} ({tr['kernel']}: FETCH_SIZE x {tr['fetch_correction']} + WRITE_SIZE)"
+    del d_buf, d_off, d_len, d_out
+    torch.cuda.empty_cache()
+    return leg, fails
+
+
+def config_c3(eng, stream, args, world, orc):
+    """configs[3] in the default line: one 16 MiB RDMA WRITE segmented at PMTU 4096 (4096 packets,
+    Write::handle's FIRST / MIDDLE... / LAST), compute with write_trailer (send) then verify with
+    zero_trailer (receive) per round trip; every trailer checked against the CPU restatement once.
+    Returns (leg, mismatches)."""
+    import torch
+
+    from icrc_amd import workloads
+
+    w3 = workloads.write_message(16 << 20, 4096)
+    d_buf = workloads.synthesize(eng, w3, stream=stream)
+    host0 = d_buf.cpu().numpy()
+    want = orc.compute_icrc_batch(host0, w3.off, w3.lens)
+    d_off, d_len = dev(w3.off), dev(w3.lens)
+    d_out = torch.zeros(w3.n, dtype=torch.int32, device="cuda")
+    d_ok = torch.zeros(w3.n, dtype=torch.uint8, device="cuda")
+
+    def rt():
+        eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_out.data_ptr(), True, 0, stream)
+        eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), True, 0, stream)
+
+    _, kms = time_kernel(rt, min(args.steps, 20), min(args.warmup, 5), world)
+    fails = int(np.count_nonzero(d_out.cpu().numpy().view(np.uint32) != want))
+    all_ok = bool((d_ok == 1).all().item())
+    tot3 = int(w3.lens.astype(np.uint64).sum())
+    leg = {"workload": "configs[3]: 16 MiB RDMA WRITE at PMTU 4096 (4096 packets), compute + write_trailer then "
+                       "verify + zero_trailer",
+           "packets": w3.n, "ms_per_roundtrip": round(kms, 4),
+           "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1), "all_ok": all_ok,
+           "parity_checked": w3.n, "parity_failures": fails}
+    del d_buf, d_off, d_len, d_out, d_ok
+    return leg, fails + (0 if all_ok else 1)
 
 
 def per_rank_fields(rows):
@@ -404,19 +498,22 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
     return fails, checked
 
 
-PMC_TRAFFIC_FILE = "r04_pmc_traffic.json"
+PMC_TRAFFIC_FILE = "r05_pmc_traffic.json"
+PMC_C2_FILE = "r05_pmc_c2_traffic.json"
 # the sources the C1 kernel is built from: a traffic summary taken on another build is not this one's
 KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp")
+# ... and the configs[2] kernel (the hybrid launch: oct + long-packet workgroups)
+C2_SOURCES = ("icrc_oct.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp")
 
 
-def kernel_source_hash() -> str:
-    """sha256 (16 hex digits) over the C1 kernel's sources as shipped in this tree, comments and
+def kernel_source_hash(names=KERNEL_SOURCES) -> str:
+    """sha256 (16 hex digits) over a kernel's sources as shipped in this tree, comments and
     blank lines removed (a comment edit does not orphan a traffic record; any code edit does)."""
     import hashlib
     import re
 
     h = hashlib.sha256()
-    for name in KERNEL_SOURCES:
+    for name in names:
         with open(os.path.join(ROOT, "open-rdma-driver_amd", "csrc", name), "r", encoding="utf-8") as f:
             text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
         code = [ln.split("//", 1)[0].rstrip() for ln in text.splitlines()]
@@ -425,25 +522,32 @@ def kernel_source_hash() -> str:
 LOADS_ONLY_VARIANT = 19  # A/B library: icrc_batch_kernel<.., S = 2, D = 1, loads only>, the default ring without the CRC
 
 
+def pmc_record(fname: str, sources, n: int, L):
+    """A committed PMC traffic record (profiles/<fname>) when it was taken on this exact workload
+    (n packets; L bytes each, or None for a ragged batch) AND this build of its kernel's sources
+    (kernel_source_hash); otherwise None."""
+    path = os.path.join(ROOT, "profiles", fname)
+    try:
+        with open(path) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if tr.get("packets") != n or (L is not None and tr.get("packet_bytes") != L):
+        return None
+    if tr.get("source_hash") != kernel_source_hash(sources):  # profiled on another build of the kernel
+        log(f"bench.py: profiles/{fname} is of kernel sources {tr.get('source_hash')}, this tree is "
+            f"{kernel_source_hash(sources)}: its traffic is left null")
+        return None
+    return tr
+
+
 def pmc_traffic(n: int, L: int):
     """roofline.traffic: HBM bytes per launch of the ICRC kernel from rocprofv3 PMC passes
     (FETCH_SIZE and WRITE_SIZE in separate runs of this same bench command, FETCH_SIZE corrected
     by the membench calibration; scripts/gpu_check.sh PMC=1 -> scripts/pmc_summary.py).  A bench
     process cannot read its own counters, so the committed summary is used when it was taken on
     this exact workload AND this build of the kernel (kernel_source_hash); otherwise None."""
-    path = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
-    try:
-        with open(path) as f:
-            tr = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if tr.get("packets") != n or tr.get("packet_bytes") != L:
-        return None
-    if tr.get("source_hash") != kernel_source_hash():  # profiled on another build of the kernel
-        log(f"bench.py: profiles/{PMC_TRAFFIC_FILE} is of kernel sources {tr.get('source_hash')}, this tree is "
-            f"{kernel_source_hash()}: roofline.traffic left null")
-        return None
-    return tr
+    return pmc_record(PMC_TRAFFIC_FILE, KERNEL_SOURCES, n, L)
 
 
 def _timed_loop(fn, budget: float):

@@ -28,15 +28,19 @@
  *   - The caller owns every buffer.  Synchronous calls retain no pointer; *_device calls
  *     borrow their pointers until the stream they were issued on is synchronised.
  *   - All entry points are reentrant.  Scalar calls, and host batches of at most 1024 packets and
- *     8 MiB (one message: configs[0] is 64 x 4156 B), queue on the engine's submitter: the kernel
- *     reads the packets from pinned, device-mapped host memory (the caller's own buffer when the
- *     whole span lies in one pinned allocation and every packet is 4-byte aligned, else a copy in
- *     a staging slot of the calling thread).  The submitter has four launch lanes (a stream each):
- *     a caller that finds a free lane launches its call there and waits on that stream only, so up
- *     to four calls are in flight at once (the emulator's three threads each get one); callers
- *     that find every lane busy are merged into the next launch.  Larger host batches serialise
- *     per engine on its two pipelined H2D staging buffers; device batches only enqueue on the
- *     caller's stream.  The default-engine registry is lock-protected.
+ *     8 MiB (one message: configs[0] is 64 x 4156 B), are host messages: the kernel reads the
+ *     packets from pinned, device-mapped host memory (the caller's own buffer when the whole span
+ *     lies in one pinned allocation and every packet is 4-byte aligned, else a copy in a staging
+ *     slot of the calling thread).  By default (ICRC_HOST_RING) a message is a job in the engine's
+ *     submission ring: a resident service kernel polls the ring's slots in pinned host memory (the
+ *     emulator's doorbell / descriptor-queue model, queues/send/queue.rs:66-100), so a call costs
+ *     no kernel launch; the kernel ends after 2 ms without calls and the next call starts it again,
+ *     and a job not done within 2 s fails with ICRC_ETIMEDOUT.  Up to four messages run at once
+ *     (the emulator's three threads each get one); more callers wait for a slot.  ICRC_HOST_LAUNCH
+ *     (icrc_engine_set_host_path) runs each message as a kernel launch instead, through a
+ *     four-stream submitter that merges callers beyond four into one launch.  Larger host batches
+ *     serialise per engine on its two pipelined H2D staging buffers; device batches only enqueue on
+ *     the caller's stream.  The default-engine registry is lock-protected.
  *   - Every CRC is computed by the HIP kernel on the GPU; there is no CPU fallback.  With
  *     no usable GPU the calls return ICRC_ENODEV.
  */
@@ -55,6 +59,7 @@ extern "C" {
 #define ICRC_ENOMEM (-12)  /* host or device allocation failed                           */
 #define ICRC_ENODEV (-19)  /* no usable GPU / engine for the requested device             */
 #define ICRC_EDEVICE (-5)  /* a HIP runtime call failed                                   */
+#define ICRC_ETIMEDOUT (-110) /* a host message's job was not done within the ring's watchdog (2 s) */
 /* PacketWriter errors (PacketProcessorError, packet_processor.rs:127-148) */
 #define ICRC_EBUFFER_NOT_LARGE (-1000) /* BufferNotLargeEnough(usize)                     */
 #define ICRC_ELENGTH_TOO_LONG (-1001)  /* LengthTooLong(usize)                            */
@@ -73,6 +78,21 @@ extern "C" {
 #define ICRC_VERIFY_BADLEN 0xFFu
 
 typedef struct icrc_engine icrc_engine;
+
+/* ---- ABI version ------------------------------------------------------------------------ */
+/* Bumped whenever a struct layout or an entry point's meaning changes.  5: icrc_write_msg is 96 bytes
+ * (88 before round 4: imm + a reserved word), the ICRC_WRITE_SEG_BY_REMOTE_VA name is gone (its bit
+ * is ICRC_WRITE_RUST_DRIVER, whose meaning grew in round 4), the submission ring. */
+#define ICRC_ABI_VERSION 5u
+uint32_t icrc_abi_version(void);
+/* A binding's start-up check: ICRC_OK when the library implements `abi_version` and the caller's
+ * struct sizes are the library's (a Rust #[repr(C)] mirror passes its size_of values), else
+ * ICRC_EINVAL — an 88-byte icrc_write_msg stride would misread every message after the first. */
+int icrc_abi_check(uint32_t abi_version, size_t write_msg_bytes, size_t rx_desc_bytes, size_t ack_ctx_bytes,
+                   size_t synth_desc_bytes);
+#define ICRC_ABI_CHECK()                                                                                  \
+    icrc_abi_check(ICRC_ABI_VERSION, sizeof(icrc_write_msg), sizeof(icrc_rx_desc), sizeof(icrc_ack_ctx), \
+                   sizeof(icrc_synth_desc))
 
 /* ---- engine lifetime ------------------------------------------------------------------ */
 /* One engine per GPU: owns the LDS table images in HBM (160 KiB each, plus a 36 KiB compact form the
@@ -98,11 +118,18 @@ void *icrc_engine_stream(const icrc_engine *engine);
  *   140 / 240  the length split as two kernels forked / joined on two streams (240: the
  *        compacting long-packet walker);
  *   301 / 302  the receive parse as one fused pass on any batch (S = 2 / S = 1).
- * Other values: ICRC_EINVAL.  The quad kernels (20, 24-26, 120-126, 220-226) and the diagnostics
- * whose results are wrong by design (15, 18, 19, 21-23, 31, 32, 35, 41-53, 141-153, 241-253)
- * exist only in the A/B library libicrc_amd_ab.so (built with ICRC_AB_BUILD), which no product
- * path loads. */
+ * Other values: ICRC_EINVAL.  The diagnostics whose results are wrong by design (15, 18, 19,
+ * 21-23, 41-53, 141-153, 241-253) exist only in the A/B library libicrc_amd_ab.so (built with
+ * ICRC_AB_BUILD), which no product path loads. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
+/* The path of host messages (scalar calls, host batches of at most 1024 packets): */
+#define ICRC_HOST_RING 0   /* the submission ring and its resident service kernel (default)         */
+#define ICRC_HOST_LAUNCH 1 /* a kernel launch per message (the four-stream submitter)               */
+int icrc_engine_set_host_path(icrc_engine *engine, int path);
+/* Counters of the engine's submission ring: out[0] jobs run, [1] service-kernel launches, [2] of
+ * them relaunches (a call after an idle exit, or a launch that ended under a job), [3] watchdog
+ * timeouts.  All zero before the first host message. */
+int icrc_engine_host_stats(icrc_engine *engine, uint64_t out[4]);
 /* Number of HIP devices visible (0 when no GPU); never fails. */
 int icrc_device_count(void);
 /* Static library/kernel description (for logs): "icrc_amd <ver> gfx950 ..." */
@@ -258,7 +285,8 @@ int icrc_synth_device(icrc_engine *engine, uint8_t *d_base, const icrc_synth_des
  * Packet s of message m is written at d_wire + m.out_offset + s * m.slot_stride; its length
  * goes to d_pkt_len[m.first_packet + s] and its ICRC to d_icrc[m.first_packet + s] (both may
  * be NULL).  Payload bytes come from d_src[m.payload_offset + segment start ...].  The
- * fast path needs (payload_offset - local_va) % 4 == 0 and out_offset, slot_stride % 4 == 0;
+ * fast path needs (payload_offset - seg_va) % 4 == 0, where seg_va is the segmentation VA
+ * (local_va; remote_va under ICRC_WRITE_RUST_DRIVER), and out_offset, slot_stride % 4 == 0;
  * other messages take a byte-wise path with identical results.  A packet longer than 65535 bytes
  * (IPv4 total length; PacketWriter::write returns LengthTooLong, packet_processor.rs:226-227) is
  * not written and reports length 0, like one that does not fit. */
@@ -319,7 +347,9 @@ typedef struct icrc_write_msg {
  *     ICRC_WRITE_ACK_REQ / _SOLICITED still set them when given.
  * PSN +1 per packet (24-bit wrap, Psn::wrapping_add, types.rs:180-183), as in both variants. */
 #define ICRC_WRITE_RUST_DRIVER 0x02u
-#define ICRC_WRITE_SEG_BY_REMOTE_VA ICRC_WRITE_RUST_DRIVER /* the round-1..3 name */
+/* (Until round 3 this bit was named ICRC_WRITE_SEG_BY_REMOTE_VA and switched only the segmentation
+ * VA.  The name is gone so that such callers fail to compile instead of silently getting the whole
+ * rust_driver rule; ICRC_ABI_VERSION 5.) */
 /* RdmaMessageMetaCommon::solicited on every packet of the message (BTH byte 1 bit 7, packet.rs:
  * 104-110); the emulator's own send paths leave it false (common.rs:90, read.rs:47). */
 #define ICRC_WRITE_SOLICITED 0x04u
@@ -337,7 +367,7 @@ typedef struct icrc_write_msg {
 #define ICRC_WRITE_NOT_LAST 0x40u
 #define ICRC_WRITE_WITH_IMM 0x80u
 /* Number of packets generate_segments_from_request yields (common.rs:152-176) for a message
- * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_SEG_BY_REMOTE_VA);
+ * whose segmentation VA is `va` (local_va, or remote_va under ICRC_WRITE_RUST_DRIVER);
  * 0 if pmtu == 0. */
 uint32_t icrc_write_segment_count(uint64_t local_va, uint32_t total_len, uint32_t pmtu);
 /* Wire length of segment s (IPv4 + UDP + BTH + RETH + payload + pad + ICRC). */
@@ -402,9 +432,6 @@ int icrc_rdma_header_len(uint8_t opcode);
  * image in HBM and the kernels replicate into LDS: the 1024 distinct bulk entries, then the final
  * tables. */
 int icrc_table_image(uint32_t *out_words, uint32_t nwords);
-/* The quad kernel's image (four packets per wavefront): M^16 bulk tables, M^(16 - (l & 15))
- * final tables, same layout. */
-int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords);
 /* The oct kernel's image (eight packets per wavefront): M^8 bulk, M^(8 - (l & 7)) final. */
 int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords);
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "icrc_internal.h"
+#include "icrc_ring.h"
 
 namespace {
 
@@ -73,7 +74,10 @@ struct Lane {
 // launch).  Packets are read by the kernel straight from pinned, device-mapped host memory (no copy
 // engine); results come back through mapped pinned memory.
 struct Combiner {
-    static constexpr int kLanes = 4;          // <= GPU_MAX_HW_QUEUES (4): one hardware queue each
+    // Four streams.  They do not own hardware queues: with GPU_MAX_HW_QUEUES = 4 HIP shares the
+    // process's four queues among every stream (these, the engine's, the staging and the callers'
+    // streams), so a lane's launch can queue behind another stream's kernel on the same queue.
+    static constexpr int kLanes = 4;
     static constexpr uint32_t kCap = 4096;    // array capacity per lane
     std::mutex mu;
     std::condition_variable cv;
@@ -84,6 +88,29 @@ struct Combiner {
                           // host allocations; the oct kernel reads a short packet's rows up to its block end)
 };
 
+// The submission ring's device side (icrc_ring.h RingDevice): the service kernel on a stream of its
+// own.  That stream is created with a CU mask (every CU) because a CU-masked stream gets a hardware
+// queue of its own: a resident kernel on a queue that another stream shares would hold that stream's
+// later kernels behind it.
+struct RingHip final : icrc::RingDevice {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool dedicated = false;  // the stream was created with a CU mask
+    icrc::RingParams rp{};
+    uint32_t nslots = 0;
+    int launch(uint32_t epoch) override;
+    int ended() override;
+};
+struct RingState {
+    RingHip dev;
+    void *host = nullptr;        // the coherent mapped block (slots, done / exited words, slot arrays)
+    uint8_t *d_mem = nullptr;    // device memory: exit flag | decision lines
+    std::unique_ptr<icrc::HostRing> ring;
+};
+constexpr uint64_t kRingWatchdogUs = 2000000;  // a job not done in 2 s fails with ICRC_ETIMEDOUT
+constexpr uint32_t kRingIdleTicks = 200000;    // 2 ms (s_memrealtime, 100 MHz) without a call: the kernel ends
+constexpr uint32_t kRingLifeTicks = 100000;    // 1 ms after its launch a busy kernel ends between jobs
+
 }  // namespace
 
 struct icrc_engine {
@@ -91,7 +118,6 @@ struct icrc_engine {
     int num_cu = 0;
     int variant = -1;  // -1: kDefaultVariant for strided batches, kDefaultRaggedVariant otherwise
     uint32_t *d_table = nullptr;
-    uint32_t *d_table_quad = nullptr;
     uint32_t *d_table_oct = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // the long-packet half of a split batch runs here, beside the caller's
@@ -101,6 +127,9 @@ struct icrc_engine {
     Stage st[2];
     std::mutex comb_init_mu;
     std::unique_ptr<Combiner> comb;  // scalar calls (created on first use)
+    int host_path = ICRC_HOST_RING;  // scalar calls and host messages: the submission ring or launches
+    std::mutex ring_mu;
+    std::unique_ptr<struct RingState> ring;  // the submission ring (created on first use)
 };
 
 namespace {
@@ -414,7 +443,6 @@ int host_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, con
         p.len = s.d_len;
         p.n = cnt;
         p.table = e->d_table;
-        p.table_quad = e->d_table_quad;
         p.table_oct = e->d_table_oct;
         p.trailer = 0;  // trailers are applied to the caller's host copy in finish_stage
         if (mode == icrc::kCompute) p.out = s.d_res;
@@ -458,7 +486,6 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
     p.ok = d_ok;
     p.nerr = d_nerr;
     p.table = e->d_table;
-    p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
     p.trailer = trailer ? 1 : 0;
     return dispatch(e, mode, p, stream);
@@ -594,7 +621,6 @@ void run_combined(icrc_engine *e, Lane &l, SubmitReq *const *reqs, uint32_t nreq
         p.ulen = L0;
     }
     p.table = e->d_table;
-    p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
     p.out = l.d_res;
     p.spread = 1;  // k <= cap <= #CUs x 16: one workgroup per packet up to #CUs, on the one-packet pipeline
@@ -640,21 +666,187 @@ int submit(icrc_engine *e, Combiner *c, SubmitReq &req) {
     return req.rc;
 }
 
+// ---- the submission ring (icrc_ring.h): creation, the device side, shutdown -------------------------
+int RingHip::launch(uint32_t epoch) {
+    DeviceGuard g(device);
+    if (!g.ok) return ICRC_ENODEV;
+    rp.epoch = epoch;
+    return icrc::launch_ring(rp, nslots, stream);
+}
+
+int RingHip::ended() {
+    DeviceGuard g(device);
+    const hipError_t q = hipStreamQuery(stream);
+    if (q == hipSuccess) return 1;
+    if (q == hipErrorNotReady) return 0;
+    (void)hipGetLastError();
+    return -1;
+}
+
+// Live rings, stopped at process exit: every wave ends (host memory only, no HIP call) before the
+// runtime's own teardown, which registered its handlers before ours.
+std::mutex g_ring_mu;
+std::vector<icrc::HostRing *> g_rings;
+void ring_atexit() {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    for (icrc::HostRing *r : g_rings) (void)r->stop(1000000);
+}
+
+void ring_free(icrc_engine *e) {
+    std::unique_ptr<RingState> rs;
+    {
+        std::lock_guard<std::mutex> lk(e->ring_mu);
+        rs = std::move(e->ring);
+    }
+    if (!rs) return;
+    if (rs->ring) {
+        {
+            std::lock_guard<std::mutex> lk(g_ring_mu);
+            g_rings.erase(std::remove(g_rings.begin(), g_rings.end(), rs->ring.get()), g_rings.end());
+        }
+        (void)rs->ring->stop(1000000);
+    }
+    if (rs->dev.stream) {
+        (void)hipStreamSynchronize(rs->dev.stream);
+        (void)hipStreamDestroy(rs->dev.stream);
+    }
+    if (rs->d_mem) (void)hipFree(rs->d_mem);
+    if (rs->host) (void)hipHostFree(rs->host);
+}
+
+// The engine's ring, created on first use (nullptr, with *rc, when it cannot be: the caller falls
+// back to kernel launches).
+icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
+    std::lock_guard<std::mutex> lk(e->ring_mu);
+    if (e->ring) return e->ring->ring ? e->ring->ring.get() : nullptr;
+    auto rs = std::make_unique<RingState>();
+    RingState *r = rs.get();
+    e->ring = std::move(rs);  // kept even on failure: a failed set-up is not retried per call
+    uint32_t nslots = icrc::kRingSlots, wgs = icrc::kRingWgPerSlot;
+    // measurement knobs (scripts/msg_probe): the ring's shape
+    if (const char *v = std::getenv("ICRC_RING_SLOTS")) nslots = static_cast<uint32_t>(std::max(1, std::min(16, std::atoi(v))));
+    if (const char *v = std::getenv("ICRC_RING_WGS")) wgs = static_cast<uint32_t>(std::max(1, std::min(32, std::atoi(v))));
+    wgs = std::min<uint32_t>(wgs, std::max<uint32_t>(1u, static_cast<uint32_t>(e->num_cu) / nslots));
+    // one coherent, device-mapped block: slot lines | done words | exited words | per slot (off, len, res)
+    const size_t words = static_cast<size_t>(nslots) * wgs;  // one done / exited word per workgroup
+    const size_t o_done = nslots * sizeof(icrc::RingSlot), o_exit = o_done + words * 4u;
+    const size_t o_arr = (o_exit + words * 4u + 255u) & ~size_t(255);
+    const size_t per_slot = icrc::kRingMaxPackets * (8u + 4u + 4u);
+    const size_t bytes = o_arr + nslots * per_slot;
+    *rc = ICRC_ENOMEM;
+    if (hipHostMalloc(&r->host, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        r->host = nullptr;
+        return nullptr;
+    }
+    std::memset(r->host, 0, bytes);
+    void *dv = nullptr;
+    *rc = ICRC_EDEVICE;
+    if (hipHostGetDevicePointer(&dv, r->host, 0) != hipSuccess) return nullptr;
+    // device memory: the exit flag (its own 256-byte block), then one decision line per workgroup
+    const size_t d_dec = 256;
+    const size_t d_bytes = d_dec + words * sizeof(icrc::RingSlot);
+    if (hipMalloc(&r->d_mem, d_bytes) != hipSuccess) {
+        r->d_mem = nullptr;
+        return nullptr;
+    }
+    if (hipMemset(r->d_mem, 0, d_bytes) != hipSuccess) return nullptr;
+    std::vector<uint32_t> mask((static_cast<size_t>(e->num_cu) + 31u) / 32u, 0u);
+    for (int cu = 0; cu < e->num_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    if (hipExtStreamCreateWithCUMask(&r->dev.stream, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess) {
+        r->dev.dedicated = true;
+    } else {
+        (void)hipGetLastError();
+        if (hipStreamCreateWithFlags(&r->dev.stream, hipStreamNonBlocking) != hipSuccess) {
+            r->dev.stream = nullptr;
+            return nullptr;
+        }
+    }
+    uint8_t *h = static_cast<uint8_t *>(r->host);
+    const uint64_t d = reinterpret_cast<uint64_t>(dv);
+    icrc::RingMemory mem;
+    mem.slots = reinterpret_cast<icrc::RingSlot *>(h);
+    mem.done = reinterpret_cast<uint32_t *>(h + o_done);
+    mem.exited = reinterpret_cast<uint32_t *>(h + o_exit);
+    mem.d_slots = d;
+    for (uint32_t s = 0; s < nslots; ++s) {
+        const size_t b = o_arr + s * per_slot;
+        mem.off[s] = reinterpret_cast<uint64_t *>(h + b);
+        mem.len[s] = reinterpret_cast<uint32_t *>(h + b + icrc::kRingMaxPackets * 8u);
+        mem.res[s] = reinterpret_cast<uint32_t *>(h + b + icrc::kRingMaxPackets * 12u);
+        mem.d_off[s] = d + b;
+        mem.d_len[s] = d + b + icrc::kRingMaxPackets * 8u;
+        mem.d_res[s] = d + b + icrc::kRingMaxPackets * 12u;
+    }
+    r->dev.device = e->device;
+    r->dev.nslots = nslots;
+    r->dev.rp.slots = reinterpret_cast<const icrc::RingSlot *>(d);
+    r->dev.rp.done = reinterpret_cast<uint32_t *>(d + o_done);
+    r->dev.rp.exited = reinterpret_cast<uint32_t *>(d + o_exit);
+    r->dev.rp.exit_flag = reinterpret_cast<uint32_t *>(r->d_mem);
+    r->dev.rp.decision = reinterpret_cast<icrc::RingSlot *>(r->d_mem + d_dec);
+    r->dev.rp.table = e->d_table;
+    r->dev.rp.wg_per_slot = wgs;
+    r->dev.rp.idle_ticks = kRingIdleTicks;
+    r->dev.rp.life_ticks = kRingLifeTicks;
+    r->ring = std::make_unique<icrc::HostRing>(&r->dev, mem, nslots, wgs, kRingWatchdogUs);
+    {
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(ring_atexit); });
+        std::lock_guard<std::mutex> gl(g_ring_mu);
+        g_rings.push_back(r->ring.get());
+    }
+    *rc = ICRC_OK;
+    return r->ring.get();
+}
+
+// One host message (n packets at dbase, the device view of pinned host memory; off / len host
+// arrays relative to dbase) -> n ICRCs into res: through the submission ring, or (host path
+// ICRC_HOST_LAUNCH, or a ring that cannot run) one launch through the four-lane submitter.  A
+// ring watchdog timeout fails the call (ICRC_ETIMEDOUT).
+int host_job(icrc_engine *e, const uint8_t *dbase, const uint64_t *off, const uint32_t *len, uint32_t n,
+             uint32_t *res) {
+    int rc = ICRC_OK;
+    if (e->host_path == ICRC_HOST_RING && n <= icrc::kRingMaxPackets) {
+        icrc::HostRing *ring = ring_for(e, &rc);
+        if (ring && !ring->retired()) {
+            icrc::RingJob j;
+            j.n = n;
+            j.res = res;
+            // equal, evenly spaced packets (a WRITE's full-MTU segments, one packet): strided
+            const uint64_t st = n > 1 ? off[1] - off[0] : len[0];
+            bool uniform = n == 1 || off[1] >= off[0];
+            for (uint32_t i = 1; uniform && i < n; i++) uniform = len[i] == len[0] && off[i] == off[0] + i * st;
+            if (uniform) {
+                j.dbase = reinterpret_cast<uint64_t>(dbase) + off[0];
+                j.stride = st;
+                j.ulen = len[0];
+            } else {
+                j.dbase = reinterpret_cast<uint64_t>(dbase);
+                j.off = off;
+                j.len = len;
+            }
+            rc = ring->submit(j);
+            if (rc != ICRC_EDEVICE) return rc;  // done, or the watchdog: the call fails
+        }
+    }
+    Combiner *c = combiner(e, &rc);
+    if (!c) return rc;
+    SubmitReq req{dbase, off, len, n, res};
+    return submit(e, c, req);
+}
+
 int scalar_call(const uint8_t *pkt, size_t len, uint32_t *result) {
     icrc_engine *e = nullptr;
     int rc = icrc_engine_default(-1, &e);
     if (rc) return rc;
     DeviceGuard g(e->device);
     if (!g.ok) return ICRC_ENODEV;
-    Combiner *c = combiner(e, &rc);
-    if (!c) return rc;
     uint8_t *h = nullptr, *d = nullptr;
     if ((rc = stage_slot(e, len, &h, &d)) != ICRC_OK) return rc;
     std::memcpy(h, pkt, len);
     const uint64_t off0 = 0;
     const uint32_t len32 = static_cast<uint32_t>(len);
-    SubmitReq req{d, &off0, &len32, 1, result};
-    return submit(e, c, req);
+    return host_job(e, d, &off0, &len32, 1, result);
 }
 
 // Device view of [base + smin, base + smax) when that whole span lies inside ONE pinned host
@@ -697,9 +889,8 @@ int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, 
     DeviceGuard g(e->device);
     if (!g.ok) return ICRC_ENODEV;
     int rc = ICRC_OK;
-    Combiner *c = combiner(e, &rc);
-    if (!c) return rc;
-    if (n > c->cap) return 1;  // a device with fewer than 64 CUs: more packets than one launch takes
+    // the submitter's launches stay at most #CUs x 16 packets (one packet per wave)
+    if (n > std::min<uint32_t>(Combiner::kCap, static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup)) return 1;
     thread_local std::vector<uint64_t> t_off;
     thread_local std::vector<uint32_t> t_res;
     t_off.resize(n);
@@ -724,8 +915,7 @@ int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, 
         }
         dbase = d;
     }
-    SubmitReq req{dbase, t_off.data(), len, n, t_res.data()};
-    if ((rc = submit(e, c, req)) != ICRC_OK) return rc;
+    if ((rc = host_job(e, dbase, t_off.data(), len, n, t_res.data())) != ICRC_OK) return rc;
     for (uint32_t i = 0; i < n; i++) {
         uint8_t *t = base + off[i] + len[i] - 4;
         const uint32_t crc = t_res[i];
@@ -753,7 +943,7 @@ extern "C" {
 
 const char *icrc_version(void) {
 #ifdef ICRC_AB_BUILD
-#define ICRC_BUILD_KIND " [A/B build: quad kernels + diagnostics]"
+#define ICRC_BUILD_KIND " [A/B build: diagnostics]"
 #else
 #define ICRC_BUILD_KIND ""
 #endif
@@ -762,6 +952,37 @@ const char *icrc_version(void) {
            "per-lane nibble tables, prefetch rings, register-buffered results, verify by CRC-32 residue"
            ICRC_BUILD_KIND;
 #undef ICRC_BUILD_KIND
+}
+
+uint32_t icrc_abi_version(void) { return ICRC_ABI_VERSION; }
+
+int icrc_abi_check(uint32_t abi_version, size_t write_msg_bytes, size_t rx_desc_bytes, size_t ack_ctx_bytes,
+                   size_t synth_desc_bytes) {
+    return abi_version == ICRC_ABI_VERSION && write_msg_bytes == sizeof(icrc_write_msg) &&
+                   rx_desc_bytes == sizeof(icrc_rx_desc) && ack_ctx_bytes == sizeof(icrc_ack_ctx) &&
+                   synth_desc_bytes == sizeof(icrc_synth_desc)
+               ? ICRC_OK
+               : ICRC_EINVAL;
+}
+
+int icrc_engine_set_host_path(icrc_engine *e, int path) {
+    if (!e || (path != ICRC_HOST_RING && path != ICRC_HOST_LAUNCH)) return ICRC_EINVAL;
+    e->host_path = path;
+    return ICRC_OK;
+}
+
+int icrc_engine_host_stats(icrc_engine *e, uint64_t out[4]) {
+    if (!e || !out) return ICRC_EINVAL;
+    out[0] = out[1] = out[2] = out[3] = 0;
+    std::lock_guard<std::mutex> lk(e->ring_mu);
+    if (e->ring && e->ring->ring) {
+        const icrc::RingStats s = e->ring->ring->stats();
+        out[0] = s.jobs;
+        out[1] = s.launches;
+        out[2] = s.relaunches;
+        out[3] = s.timeouts;
+    }
+    return ICRC_OK;
 }
 
 int icrc_device_count(void) {
@@ -797,16 +1018,6 @@ int icrc_engine_create(int device, icrc_engine **out) {
     icrc::append_compact_image(img.data());
     icrc::build_table_image_oct(img_oct.data());
     icrc::append_compact_image(img_oct.data());
-#ifdef ICRC_AB_BUILD  // the quad kernels' image (A/B library only)
-    std::vector<uint32_t> img_quad(icrc::kTableBufWords);
-    icrc::build_table_image_quad(img_quad.data());
-    icrc::append_compact_image(img_quad.data());
-    if (hipMalloc(&e->d_table_quad, kBufBytes) != hipSuccess ||
-        hipMemcpy(e->d_table_quad, img_quad.data(), kBufBytes, hipMemcpyHostToDevice) != hipSuccess) {
-        icrc_engine_destroy(e);
-        return ICRC_EDEVICE;
-    }
-#endif
     if (hipMalloc(&e->d_table, kBufBytes) != hipSuccess ||
         hipMemcpy(e->d_table, img.data(), kBufBytes, hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc(&e->d_table_oct, kBufBytes) != hipSuccess ||
@@ -828,10 +1039,10 @@ int icrc_engine_destroy(icrc_engine *e) {
         DeviceGuard g(e->device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
         if (e->side) (void)hipStreamSynchronize(e->side);
+        ring_free(e);
         for (Stage &s : e->st) stage_free(s);
         combiner_free(e);
         if (e->d_table) (void)hipFree(e->d_table);
-        if (e->d_table_quad) (void)hipFree(e->d_table_quad);
         if (e->d_table_oct) (void)hipFree(e->d_table_oct);
         if (e->stream) (void)hipStreamDestroy(e->stream);
         if (e->side) (void)hipStreamDestroy(e->side);
@@ -1015,7 +1226,6 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     // Otherwise two passes (icrc_kernels.hip, icrc_rx_desc_kernel): the verify dispatch writes the
     // ok bytes (into d_ok, or a stream-ordered scratch array when the caller passes none), then the
     // descriptors are built from the header words and those bytes.
-    p.table_quad = e->d_table_quad;
     p.table_oct = e->d_table_oct;
     uint8_t *scratch = nullptr;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1095,13 +1305,6 @@ int icrc_write_packetize_device(icrc_engine *e, const uint8_t *d_src, uint64_t s
 int icrc_table_image(uint32_t *out_words, uint32_t nwords) {
     if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
     icrc::build_table_image(out_words);
-    if (nwords >= icrc::kTableBufWords) icrc::append_compact_image(out_words);  // the device buffer
-    return ICRC_OK;
-}
-
-int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords) {
-    if (!out_words || nwords < icrc::kLdsWords) return ICRC_EINVAL;
-    icrc::build_table_image_quad(out_words);
     if (nwords >= icrc::kTableBufWords) icrc::append_compact_image(out_words);  // the device buffer
     return ICRC_OK;
 }

@@ -1,4 +1,4 @@
-// icrc_device.h — device helpers shared by the HIP kernels (icrc_kernels.hip, icrc_quad.hip).
+// icrc_device.h — device helpers shared by the HIP kernels (icrc_kernels.hip, icrc_oct.hip).
 // Included inside namespace icrc { namespace { ... } } of each translation unit.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -355,7 +355,7 @@ __device__ __forceinline__ void table_fill(uint4 *lds4, const uint32_t *table) {
 
 constexpr int kStreamAux = 2;  // nt: packets are read once (MI355X_MICROARCH.md nt-weights); +7 % on C1
 
-// ---- helpers of the multi-packet-per-wave kernels (icrc_quad.hip, icrc_oct.hip) ----------------
+// ---- helpers of the multi-packet-per-wave kernel (icrc_oct.hip) ----------------------------------
 __device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
 }
@@ -378,7 +378,7 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t x) {
 
 // Generic per-packet path on the W-lane tables (group 0 computes; wave-uniform result).
 template <int MODE, int W>
-__device__ __forceinline__ uint32_t quad_slow_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
+__device__ __forceinline__ uint32_t group_slow_packet(const BatchParams &p, uint8_t *pkt, uint32_t L, const char *lds,
                                                      const LaneConsts &c, uint32_t lane) {
     if (L < ICRC_MIN_PACKET) {
         if (lane == 0 && p.nerr) atomicAdd(p.nerr, 1u);

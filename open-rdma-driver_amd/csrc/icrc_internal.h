@@ -19,11 +19,6 @@ constexpr uint32_t kLdsWords = kLdsBytes / 4;
 
 // Host: fill a kLdsWords image.
 void build_table_image(uint32_t *img);
-// Quad image (the 4-packets-per-wavefront kernel, 16 lanes = 16 stream words per packet row):
-// the same layout with M^16 in the bulk tables and, for lane l, M^(16 - (l & 15)) in the
-// final tables — so the final lookup of lane l = 16 g + c is conflict-free across the 4
-// packet groups g (bank (16 g + c) of each 256-byte table row).
-void build_table_image_quad(uint32_t *img);
 // Oct image (eight packets per wavefront, 8 lanes each): M^8 bulk, M^(8 - (l & 7)) final.
 void build_table_image_oct(uint32_t *img);
 // Compact image, stored in HBM right after each full image (the device buffer holds
@@ -69,9 +64,8 @@ struct BatchParams {
     int trailer;     // compute: write trailer; verify: zero trailer
     int variant;     // kernel variant (icrc_kernels.hip launch_mode): 0 = unpipelined, 1..5 = pipelined
     icrc_rx_desc *rx;  // receive parse (launch_rx): one descriptor per packet
-    const uint32_t *table_quad;  // kLdsWords quad image (W = 16: variants 19-23)
-    const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 24-35)
-    uint32_t split_len;  // hybrid dispatch (0 = off): the quad kernel takes L < split_len, the
+    const uint32_t *table_oct;   // kLdsWords oct image (W = 8: variants 40-53)
+    uint32_t split_len;  // hybrid dispatch (0 = off): the oct kernel takes L < split_len, the
                          // long-packet kernel (launch_long) L >= split_len
     int long_variant;    // launch_long: 0 = filtered S = 2 pipeline (default), 1 = compacting S = 1 walker
     int spread;          // one-packet pipeline: consecutive waves' packets on different workgroups
@@ -82,10 +76,7 @@ struct BatchParams {
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)
 constexpr int kDefaultRaggedVariant = 40;  // oct, fixed 10-row frames (icrc_oct.hip): L <= 320
 constexpr int kOctVariant = 40;
-// Hybrid dispatch threshold: shorter packets go to the oct kernel (per-packet costs / 8), longer
-// ones to the one-packet pipeline (one contiguous row per wave instruction streams faster).
-constexpr uint32_t kSplitLen = 2048;
-// 100 + q (q a quad / oct variant): the default hybrid dispatch with q as its short-packet kernel.
+// 100 + q (q an oct variant): the default hybrid dispatch with q as its short-packet kernel.
 constexpr int kHybridVariantBase = 100;
 // 200 + q: the same with the compacting long-packet walker (A/B); 301: the fused single-pass
 // receive parse (A/B against the two-pass default).
@@ -94,20 +85,20 @@ constexpr int kRxVariantBase = 300;
 // Variants a batch can be forced to (icrc_engine_set_kernel_variant).  The product library
 // accepts only result-exact ones: 0, 13, 16, 17 (one packet per wave) and 40 (oct).  The A/B
 // library (built with ICRC_AB_BUILD: _build/libicrc_amd_ab.so, for measurement scripts and the
-// bench's loads-only denominator) adds the quad kernels 20, 24-26 (icrc_quad.hip) and the
-// diagnostics 15, 18, 19, 21-23, 31, 32, 35, 41-53, whose results are wrong by design (49 and 51 are
-// exact on strided batches only / on all batches, 48, 52 and 53 exact, but ablations all the same).
+// bench's loads-only denominator) adds the diagnostics 15, 18, 19, 21-23, 41-53, whose results are
+// wrong by design (49 and 51 are exact on strided batches only / on all batches, 48, 52 and 53
+// exact, but ablations all the same).
 #ifdef ICRC_AB_BUILD
 inline bool is_batch_variant(int v) {
     switch (v) {
-    case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 31: case 32: case 35:
+    case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 21: case 22: case 23:
     case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51: case 52: case 53:
         return true;
     default:
         return false;
     }
 }
-inline bool is_short_variant(int v) { return v == 20 || v == 24 || v == 25 || v == 26 || (v >= 40 && v <= 53); }
+inline bool is_short_variant(int v) { return v >= 40 && v <= 53; }
 #else
 inline bool is_batch_variant(int v) { return v == 0 || v == 13 || v == 16 || v == 17 || v == 40; }
 inline bool is_short_variant(int v) { return v == 40; }
@@ -126,18 +117,15 @@ int launch_rx(const BatchParams &p, int grid, void *stream);  // fused verify + 
 // Receive parse pass 2 (the default path): descriptors from the header words, icrc_ok read from
 // p.ok where the verify pass left it.
 int launch_rx_desc(const BatchParams &p, int num_cu, void *stream);
-// Quad / chunked oct kernels (icrc_quad.hip, A/B library only), variants 20, 24-26 (and
-// diagnostics 31, 32, 35).
-int launch_quad(int mode, int variant, const BatchParams &p, int grid, void *stream);
 // Fixed-frame oct kernel (icrc_oct.hip), variant 40: packets of at most oct_max_len() bytes.
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag = 0);
 uint32_t oct_max_len();
 // The hybrid dispatch with the oct kernel as its short-packet half, in one launch (icrc_oct.hip):
 // grid_oct workgroups of the oct kernel, then grid_long of the long-packet kernel.
 int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);
-// The length from which the hybrid dispatch hands packets to the long-packet kernel, for the
-// short-packet variant v: what the fixed-frame oct kernel can hold, else kSplitLen.
-inline uint32_t split_len_for(int v) { return v >= kOctVariant && v <= kOctVariant + 13 ? oct_max_len() + 1u : kSplitLen; }
+// The length from which the hybrid dispatch hands packets to the long-packet kernel: what the
+// fixed-frame oct kernel can hold.
+inline uint32_t split_len_for(int) { return oct_max_len() + 1u; }
 int launch_synth(uint8_t *base, const icrc_synth_desc *desc, const uint8_t *hdr, uint32_t n,
                  void *stream);
 struct PacketizeParams {
@@ -157,6 +145,55 @@ int launch_ack(const icrc_rx_desc *desc, const icrc_ack_ctx *ctx, uint32_t n, ui
                uint32_t *out_len, uint32_t mode, int num_cu, void *stream);
 int launch_ipv4_checksum(uint8_t *base, const uint64_t *off, uint64_t stride, uint32_t n, uint16_t *csum, int fill,
                          void *stream);
+
+// ---- host-message submission ring (icrc_ring.cpp: host protocol; icrc_ring_kernel: service) ----
+// The emulator's own call model is a doorbell and a queue its send thread drains
+// (blue-rdma-device/src/queues/send/queue.rs:66-100, rust_driver/src/device/ringbuf.rs:201-209).
+// Here: a resident service kernel keeps the W = 64 tables in LDS and polls a ring of job slots in
+// coherent pinned host memory; a host caller fills a free slot (one message: a scalar packet or a
+// host batch of at most kRingMaxPackets) and publishes it by writing the slot's cmd word last.
+// Slot s is served by kRingWgPerSlot workgroups.  While idle only wave 0 of each workgroup runs: it
+// polls the slot's line, and on a new job writes it into its workgroup's decision line in device
+// memory; the workgroup then takes its share of the job in lockstep (a barrier before and after)
+// and its wave 0 writes the cmd into the workgroup's done word, so the host sees completion without
+// any atomic.  The kernel ends when the
+// host sets kRingStop, or when a leader has seen no call for RingParams::idle_ticks or has run for
+// life_ticks (it sets the exit flag, which every workgroup polls between jobs: one leader ends them all,
+// so a half-alive kernel never holds a slot); the host relaunches it on the next call, and re-runs a job
+// whose launch ended under it.
+constexpr uint32_t kRingStop = 0x80000000u;  // RingSlot::cmd: every wave exits
+constexpr uint32_t kRingMaxPackets = 1024u;  // packets per job (one message)
+constexpr uint32_t kRingMaxSlots = 16u;
+constexpr uint32_t kRingSlots = 4u;          // default: one per emulator thread (3) + one
+constexpr uint32_t kRingWgPerSlot = 8u;      // default workgroups per slot (CUs reading one message)
+struct alignas(64) RingSlot {  // host-written, one 64-byte line per slot
+    uint32_t cmd;       // job number (bits 0-30, never 0 for a job) | kRingStop; written last
+    uint32_t activity;  // the host's submission counter, copied into every slot on every call
+    uint32_t n;         // packets
+    uint32_t ulen;      // uniform length (packet i at base + i * stride) or 0 (off / len arrays)
+    uint64_t base;      // device address of the packet bytes (mapped host memory)
+    uint64_t stride;
+    uint64_t off;       // device address of n u64 offsets from base (ulen == 0)
+    uint64_t len;       // device address of n u32 lengths (ulen == 0)
+    uint64_t out;       // device address of n u32 ICRCs (coherent mapped host memory)
+    uint32_t rsvd[2];
+};
+static_assert(sizeof(RingSlot) == 64, "one line per slot");
+struct RingParams {
+    const RingSlot *slots;  // device view of the slot lines (host memory)
+    uint32_t *done;         // [slot][wg]: the last cmd each workgroup finished (host memory)
+    uint32_t *exited;       // [slot][wg]: epoch, stored when the workgroup ends (host memory)
+    uint32_t *exit_flag;    // device memory: epoch once a leader has timed out
+    RingSlot *decision;     // device memory [slot][wg]: wave 0's decision (the job, or kRingStop)
+    const uint32_t *table;  // W = 64 table buffer (image + compact form)
+    uint32_t wg_per_slot;
+    uint32_t epoch;         // launch number
+    uint32_t idle_ticks;    // s_memrealtime ticks (100 MHz) without host activity before exiting
+    uint32_t life_ticks;    // ... and since the launch: a launch ends at a job boundary after this long,
+                            // so a kernel that needs every CU (the batch kernels: one 160 KiB workgroup
+                            // per CU) waits at most that long for the CUs the ring holds
+};
+int launch_ring(const RingParams &rp, uint32_t nslots, void *stream);
 
 // Segmentation shared by host and tests (generate_segments_from_request, common.rs:152-176).
 inline uint32_t write_first_segment(uint64_t local_va, uint32_t total_len, uint32_t pmtu) {

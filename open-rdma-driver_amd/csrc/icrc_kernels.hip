@@ -816,9 +816,8 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 // Variants: 0 one packet per wave, no pipelining; 13 one chain per wave (S = 1, D = 1); 16 two
 // chains (S = 2, D = 1, the default for long packets); 15 / 18 diagnostics of the S = 1, D = 2
 // shape (loads only / CRC only: wrong results by design); 19 loads only of variant 16's ring; 17
-// variant 16 without the raised wave priority around its load bursts; 20, 24-26, 31, 32, 35: the quad /
-// chunked oct kernels (icrc_quad.hip); 40: the fixed-frame oct kernel (icrc_oct.hip, default
-// for short packets).
+// variant 16 without the raised wave priority around its load bursts; 40: the fixed-frame oct kernel
+// (icrc_oct.hip, default for short packets).
 using RingNt = Ring<kStreamAux>;
 using RingNtNoPrio = Ring<kStreamAux, false>;
 #ifdef ICRC_AB_BUILD
@@ -835,20 +834,13 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 13: ICRC_LAUNCH_T(1, 1, RingNt); break;        // S = 1, nt row loads
     case 17: ICRC_LAUNCH_T(2, 1, RingNtNoPrio); break;  // 16 without the raised priority (A/B)
     case 40: (void)launch_oct(MODE, p, grid, s); break;
-#ifdef ICRC_AB_BUILD  // the A/B library only: quad kernels and diagnostics (wrong results by design)
+#ifdef ICRC_AB_BUILD  // the A/B library only: diagnostics (wrong results by design)
     case 15: ICRC_LAUNCH(1, 2, RingLoadsOnly, false); break;  // loads only, nt
     case 18: ICRC_LAUNCH(1, 2, RingCrcOnly, false); break;   // CRC only (as 15)
     case 19: ICRC_LAUNCH(2, 1, RingLoadsOnly, false); break;  // loads only of 16's ring
     case 21: ICRC_LAUNCH(2, 1, RingNoFinal, false); break;   // 16 without final products
     case 22: ICRC_LAUNCH(2, 1, RingNoStore, false); break;   // 16 without result stores
     case 23: ICRC_LAUNCH(2, 1, RingBare, false); break;      // 19 without final products and stores
-    case 20:
-    case 24:
-    case 25:
-    case 26:
-    case 31:
-    case 32:
-    case 35: (void)launch_quad(MODE, p.variant, p, grid, s); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products

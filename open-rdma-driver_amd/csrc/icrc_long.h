@@ -678,10 +678,10 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 
 // ---- long packets of a ragged batch (hybrid dispatch) ------------------------------------------
 // The one-packet pipeline (S = 1, D-deep prefetch) over only the packets with L >= p.split_len;
-// the quad kernel (icrc_quad.hip) takes the shorter ones, whose per-packet costs it divides by
-// four.  Long packets stay here because one contiguous 256-byte row per wave instruction
-// streams from HBM at ~6.2 TB/s, while four packets per instruction stop at ~4.5 TB/s
-// (profiles/r01_membench.json, patterns D and E).  The walk skips short packets with the
+// the oct kernel (icrc_oct.hip) takes the shorter ones, whose per-packet costs it divides by
+// eight.  Long packets stay here because one contiguous 256-byte row per wave instruction
+// streams from HBM faster than several packets per instruction (profiles/r01_membench.json,
+// patterns D and E; profiles/r02_shortbench.jsonl).  The walk skips short packets with the
 // ballot of each 64-packet meta block; results are kept per block and stored 64 at a time.
 // Packets in flight ahead of the one being stepped (3 measured the same on C2: the long half's
 // tail is the CUs freeing up from the short-packet kernel, not the walk's latency).

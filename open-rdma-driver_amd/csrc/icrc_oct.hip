@@ -640,7 +640,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 const uint64_t o = static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off), l)) |
                                    (static_cast<uint64_t>(readlane_u32(static_cast<uint32_t>(off >> 32), l)) << 32);
                 const uint32_t Ll = readlane_u32(L, l);
-                const uint32_t r = quad_slow_packet<MODE, 8>(p, p.base + o, Ll, lds, c, lane);
+                const uint32_t r = group_slow_packet<MODE, 8>(p, p.base + o, Ll, lds, c, lane);
                 if (lane == 0) store_result<MODE>(p, lo + static_cast<uint32_t>(b) * 64u + static_cast<uint32_t>(l), r);
             }
         }

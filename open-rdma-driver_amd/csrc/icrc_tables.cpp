@@ -51,7 +51,7 @@ uint32_t advance_words(uint32_t state, uint32_t nwords) {
     return state;
 }
 
-// Row width W words (64: one packet per wavefront; 16: four packets per wavefront).
+// Row width W words (64: one packet per wavefront; 8: eight packets per wavefront).
 static void build_image(uint32_t *img, uint32_t W) {
     std::memset(img, 0, kLdsBytes);
     const Matrix mb = matrix_pow(W);
@@ -83,8 +83,6 @@ void append_compact_image(uint32_t *img) {
 }
 
 void build_table_image(uint32_t *img) { build_image(img, 64); }
-
-void build_table_image_quad(uint32_t *img) { build_image(img, 16); }
 
 void build_table_image_oct(uint32_t *img) { build_image(img, 8); }
 

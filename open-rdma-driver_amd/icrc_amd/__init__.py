@@ -24,8 +24,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ICRC_AMD_LIB: another build of the same library (A/B measurements of two builds in one run)
 LIB_PATH = os.environ.get("ICRC_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd.so")
-# The A/B library: the same sources built with ICRC_AB_BUILD (quad kernels + diagnostic variants
-# whose results are wrong by design).  Loaded only on request (ab_library()), never by the product
+# The A/B library: the same sources built with ICRC_AB_BUILD (diagnostic variants whose results
+# are wrong by design).  Loaded only on request (ab_library()), never by the product
 # path.
 AB_LIB_PATH = os.environ.get("ICRC_AMD_AB_LIB") or os.path.join(os.path.dirname(_HERE), "_build", "libicrc_amd_ab.so")
 
@@ -34,6 +34,9 @@ EINVAL = -22
 ENOMEM = -12
 ENODEV = -19
 EDEVICE = -5
+ETIMEDOUT = -110
+ABI_VERSION = 5  # ICRC_ABI_VERSION (include/icrc.h)
+HOST_RING, HOST_LAUNCH = 0, 1  # icrc_engine_set_host_path
 EBUFFER_NOT_LARGE = -1000
 ELENGTH_TOO_LONG = -1001
 EINVALID_METADATA = -1002
@@ -103,7 +106,6 @@ WRITE_MSG_DTYPE = np.dtype([
     ("imm", "<u4"), ("_rsvd", "<u4"),
 ])
 WRITE_FILL_IPV4_CSUM, WRITE_RUST_DRIVER, WRITE_SOLICITED, WRITE_ACK_REQ = 0x01, 0x02, 0x04, 0x08
-WRITE_SEG_BY_REMOTE_VA = WRITE_RUST_DRIVER  # BlueRDMALogic::send (logic.rs:168-271), see include/icrc.h
 WRITE_UDP_PAYLOAD_ONLY = 0x10  # BTH .. ICRC at each slot (generate_payload_from_msg's form)
 # ToCardWriteDescriptor is_first = false / is_last = false / WriteWithImm (types.rs:548-555, 641-648)
 WRITE_NOT_FIRST, WRITE_NOT_LAST, WRITE_WITH_IMM = 0x20, 0x40, 0x80
@@ -166,7 +168,6 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
                                             ctypes.c_uint16, ctypes.c_uint16]),
         "icrc_rdma_header_len": (i32, [ctypes.c_uint8]),
         "icrc_table_image": (i32, [vp, u32]),
-        "icrc_table_image_quad": (i32, [vp, u32]),
         "icrc_table_image_oct": (i32, [vp, u32]),
         "icrc_write_segment_count": (u32, [u64, u32, u32]),
         "icrc_write_packet_len": (u32, [u64, u32, u32, u32]),
@@ -174,6 +175,11 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "icrc_rx_parse_device": (i32, [vp, vp, vp, vp, u64, u32, u32, vp, vp, i32, vp, vp]),
         "icrc_ipv4_checksum_device": (i32, [vp, vp, vp, u64, u32, vp, i32, vp]),
         "icrc_ack_from_rx_device": (i32, [vp, vp, vp, u32, vp, u32, vp, u32, vp]),
+        "icrc_abi_version": (u32, []),
+        "icrc_abi_check": (i32, [u32, sz, sz, sz, sz]),
+        "icrc_engine_set_host_path": (i32, [vp, i32]),
+        "icrc_engine_host_stats": (i32, [vp, ctypes.POINTER(u64)]),
+        "icrc_ring_selftest": (i32, [i32, i32, i32]),  # test hook, not in include/icrc.h
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -235,10 +241,10 @@ COMPACT_WORDS = 1024 + 8192  # kCompactWords: 1024 bulk entries + the 32 KiB fin
 
 def table_image(width: int = 64, compact: bool = False) -> np.ndarray:
     """The LDS table image the kernels upload for rows of `width` words: 64 (one packet per
-    wavefront), 16 (quad: four packets per wavefront) or 8 (oct: eight).  compact: followed by
+    wavefront) or 8 (oct: eight packets per wavefront).  compact: followed by
     the compact form the engine keeps after it in HBM (what the kernels replicate into LDS)."""
     img = np.zeros(LDS_WORDS + (COMPACT_WORDS if compact else 0), dtype=np.uint32)
-    fn = {64: lib.icrc_table_image, 16: lib.icrc_table_image_quad, 8: lib.icrc_table_image_oct}[width]
+    fn = {64: lib.icrc_table_image, 8: lib.icrc_table_image_oct}[width]
     _check(fn(img.ctypes.data, img.size), "icrc_table_image")
     return img
 
@@ -353,6 +359,36 @@ def verify_icrc_batch(base: np.ndarray, off, lens, zero_trailer: bool = False) -
     return ok
 
 
+def _default_engine(device: int = -1) -> ctypes.c_void_p:
+    h = ctypes.c_void_p()
+    _check(lib.icrc_engine_default(device, ctypes.byref(h)), "icrc_engine_default")
+    return h
+
+
+def set_host_path(path: int, device: int = -1) -> None:
+    """The default engine's host-message path (the module-level drop-ins above use it):
+    HOST_RING (default) or HOST_LAUNCH."""
+    _check(lib.icrc_engine_set_host_path(_default_engine(device), path), "icrc_engine_set_host_path")
+
+
+def host_stats(device: int = -1) -> dict:
+    """The default engine's submission-ring counters (icrc_engine_host_stats)."""
+    out = (ctypes.c_uint64 * 4)()
+    _check(lib.icrc_engine_host_stats(_default_engine(device), out), "icrc_engine_host_stats")
+    return {"jobs": out[0], "launches": out[1], "relaunches": out[2], "timeouts": out[3]}
+
+
+def abi_check() -> int:
+    """icrc_abi_check with this binding's own struct sizes (the mirrors below)."""
+    return lib.icrc_abi_check(ABI_VERSION, WRITE_MSG_DTYPE.itemsize, RX_DESC_DTYPE.itemsize, 12, SYNTH_DESC_DTYPE.itemsize)
+
+
+def ring_selftest(scenario: int, threads: int = 3, jobs_per_thread: int = 200) -> int:
+    """The submission ring's host protocol against a simulated service kernel on a CPU thread
+    (icrc_ring_selftest, a test hook of the library): 0 = the scenario behaved as specified."""
+    return lib.icrc_ring_selftest(scenario, threads, jobs_per_thread)
+
+
 class Engine:
     """One engine per GPU (icrc_engine_create).  Device entry points take raw device pointers
     (e.g. torch tensor .data_ptr()) and a hipStream_t handle (e.g.
@@ -371,6 +407,16 @@ class Engine:
     def ordinal(self) -> int:
         """The HIP device the engine runs on (icrc_engine_device_ordinal)."""
         return int(self._lib.icrc_engine_device_ordinal(self.handle))
+
+    def set_host_path(self, path: int) -> None:
+        """HOST_RING (default: the submission ring) or HOST_LAUNCH (a kernel launch per message)."""
+        _check(self._lib.icrc_engine_set_host_path(self.handle, path), "icrc_engine_set_host_path")
+
+    def host_stats(self) -> dict:
+        """The submission ring's counters (icrc_engine_host_stats)."""
+        out = (ctypes.c_uint64 * 4)()
+        _check(self._lib.icrc_engine_host_stats(self.handle, out), "icrc_engine_host_stats")
+        return {"jobs": out[0], "launches": out[1], "relaunches": out[2], "timeouts": out[3]}
 
     def set_variant(self, variant: int) -> None:
         """Kernel variant for A/B runs (0 = unpipelined, S >= 1 = S packets in flight/wave)."""
@@ -426,6 +472,15 @@ class Engine:
                                          lens.ctypes.data, off.size, out.ctypes.data,
                                          1 if write_trailer else 0), "icrc_compute_batch_ex")
         return out
+
+    def verify_batch_host(self, base: np.ndarray, off, lens, zero_trailer: bool = False) -> np.ndarray:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        ok = np.zeros(off.size, dtype=np.uint8)
+        _check(self._lib.icrc_verify_batch_ex(self.handle, _u8(base, writable=zero_trailer).ctypes.data, off.ctypes.data,
+                                        lens.ctypes.data, off.size, ok.ctypes.data,
+                                        1 if zero_trailer else 0), "icrc_verify_batch_ex")
+        return ok
 
     def rx_parse(self, d_base: int, d_off: int, d_len: int, n: int, d_desc: int, d_ok: int = 0,
                  zero_trailer: bool = False, d_nerr: int = 0, stride: int = 0, length: int = 0,

@@ -2,7 +2,7 @@
 """A/B the ICRC kernel variants in ONE process, interleaved rounds (methodology rule 24):
 C1 (1 Mi x 4156 B, strided) and C2 (mixed MTU, ragged) for each variant; checks that every
 variant returns identical ICRCs.  Prints one JSON line per (workload, variant)."""
-DIAGNOSTIC = {15, 18, 19, 21, 22, 23, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 50, 53}  # ablations (loads-only / CRC-only / no loads): wrong results by design
+DIAGNOSTIC = {15, 18, 19, 21, 22, 23, 41, 42, 43, 44, 45, 46, 47, 48, 50, 53}  # ablations (loads-only / CRC-only / no loads): wrong results by design
 import json
 import os
 import sys
@@ -28,7 +28,7 @@ def main():
     rounds = int(os.environ.get("ROUNDS", "5"))
     launches = int(os.environ.get("LAUNCHES", "10"))
     # the product library (or ICRC_AMD_LIB's build) unless a variant exists only in the A/B build
-    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (20, 24, 25, 26, 27, 49, 51, 52) for v in variants if v >= 0)
+    ab_only = any(v % 100 in DIAGNOSTIC or v % 100 in (49, 51, 52) for v in variants if v >= 0)
     eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library() if ab_only else None)
     s = torch.cuda.current_stream().cuda_stream
     jobs = {}

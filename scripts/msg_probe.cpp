@@ -5,7 +5,9 @@
 // (is_icrc_valid, packet_processor.rs:341-353).  Cases: pinned / pageable message buffers; 64
 // packets, and 1 packet (the per-call floor).  Run it under rocprofv3 --kernel-trace --stats to
 // split each call into kernel time and the rest.  Prints one JSON line per case (p50 / p99 /
-// mean microseconds per call); every verify must succeed.
+// mean microseconds per call); every verify must succeed.  MSG_PROBE_PATH=launch runs the host
+// messages as one kernel launch each (ICRC_HOST_LAUNCH) instead of through the submission ring
+// (the default); the last line is the ring's counters (icrc_engine_host_stats).
 // Build: see scripts/Makefile (links libicrc_amd.so and the HIP runtime for pinned memory).
 #include <hip/hip_runtime.h>
 
@@ -124,8 +126,30 @@ void run_threads(const char *name, const std::vector<uint8_t> &src, bool pinned_
 
 }  // namespace
 
+void print_stats(const char *path) {
+    icrc_engine *e = nullptr;
+    uint64_t st[4] = {0, 0, 0, 0};
+    if (icrc_engine_default(-1, &e) == ICRC_OK) (void)icrc_engine_host_stats(e, st);
+    printf("{\"host_path\": \"%s\", \"ring_jobs\": %llu, \"ring_launches\": %llu, \"ring_relaunches\": %llu, "
+           "\"ring_timeouts\": %llu}\n",
+           path, static_cast<unsigned long long>(st[0]), static_cast<unsigned long long>(st[1]),
+           static_cast<unsigned long long>(st[2]), static_cast<unsigned long long>(st[3]));
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     const int calls = argc > 1 ? atoi(argv[1]) : 2000;
+    const char *pv = getenv("MSG_PROBE_PATH");
+    const bool launch = pv && strcmp(pv, "launch") == 0;
+    {
+        icrc_engine *e = nullptr;
+        if (icrc_engine_default(-1, &e) != ICRC_OK ||
+            icrc_engine_set_host_path(e, launch ? ICRC_HOST_LAUNCH : ICRC_HOST_RING) != ICRC_OK) {
+            fprintf(stderr, "no engine\n");
+            return 1;
+        }
+    }
+    const char *path = launch ? "launch" : "ring";
     const uint32_t L = 4156, npk = 64;
     std::vector<uint8_t> pageable(static_cast<size_t>(npk) * L);
     uint32_t x = 12345;
@@ -144,16 +168,18 @@ int main(int argc, char **argv) {
     if (argc > 2) {  // msg_probe CALLS THREADS...: the multi-threaded message rate only
         for (int a = 2; a < argc; ++a) {
             const int T = atoi(argv[a]);
-            run_threads("pinned", pageable, true, npk, L, calls, T);
-            run_threads("pageable", pageable, false, npk, L, calls, T);
+            run_threads(launch ? "pinned, launch" : "pinned, ring", pageable, true, npk, L, calls, T);
+            run_threads(launch ? "pageable, launch" : "pageable, ring", pageable, false, npk, L, calls, T);
         }
+        print_stats(path);
         (void)hipHostFree(pinned);
         return 0;
     }
-    run("pinned", pinned, npk, L, calls);
-    run("pageable", pageable.data(), npk, L, calls);
-    run("pinned_1_packet", pinned, 1, L, calls);
-    run("pageable_1_packet", pageable.data(), 1, L, calls);
+    run(launch ? "pinned, launch" : "pinned, ring", pinned, npk, L, calls);
+    run(launch ? "pageable, launch" : "pageable, ring", pageable.data(), npk, L, calls);
+    run(launch ? "pinned_1_packet, launch" : "pinned_1_packet, ring", pinned, 1, L, calls);
+    run(launch ? "pageable_1_packet, launch" : "pageable_1_packet, ring", pageable.data(), 1, L, calls);
+    print_stats(path);
     (void)hipHostFree(pinned);
     return 0;
 }

@@ -20,7 +20,12 @@ from collections import defaultdict
 N, L = 1 << 20, 4156
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import kernel_source_hash  # noqa: E402  (sha of the kernel sources this summary describes)
+from bench import C2_SOURCES, kernel_source_hash  # noqa: E402  (sha of the kernel sources a record describes)
+
+# FETCH_SIZE per counted byte for the oct kernel's access shape (8 packets per wave, 32-byte dword
+# rows, default policy), calibrated on scripts/shortbench.hip's known byte counts: x1.983 on 316-B
+# and x1.958 on 1084-B packets (profiles/r03_pmc_c2.txt); configs[2] is 88 % 316-B-class packets.
+OCT_FETCH_CORRECTION = 1.98
 
 
 def short(name):
@@ -93,6 +98,24 @@ def main():
                 "fetch_correction": round(corr, 4), "fetch_bytes_corrected": round(fetch),
                 "write_bytes": round(write), "traffic_bytes": round(fetch + write),
                 "algorithmic_bytes": alg, "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
+    # configs[2]: the default one-launch hybrid kernel (compute, no trailer, dense / compacting long
+    # walk by density) over the 4 Mi mixed-MTU batch of bench.py's c2 leg
+    for name, d in bench.items():
+        if name.startswith("icrc_hybrid_kernel<0, false, false") and "FETCH_SIZE_KB_mean" in d:
+            sys.path.insert(0, os.path.join(ROOT, "open-rdma-driver_amd"))
+            from icrc_amd import workloads  # noqa: E402
+
+            wm = workloads.mixed_mtu_stream(4 << 20)
+            alg = int(wm.lens.astype("uint64").sum())  # L - 4 read + 4 written per packet
+            fetch = d["FETCH_SIZE_KB_mean"] * 1024.0 * OCT_FETCH_CORRECTION
+            write = d.get("WRITE_SIZE_KB_mean", 0.0) * 1024.0
+            res["c2_traffic_per_launch"] = {
+                "kernel": name, "packets": wm.n, "source_hash": kernel_source_hash(C2_SOURCES),
+                "fetch_bytes_counted": d["FETCH_SIZE_KB_mean"] * 1024.0,
+                "fetch_correction": OCT_FETCH_CORRECTION, "fetch_bytes_corrected": round(fetch),
+                "write_bytes": round(write), "traffic_bytes": round(fetch + write),
+                "algorithmic_bytes": alg, "ratio_to_algorithmic": round((fetch + write) / alg, 4),
+                "note": "the (offset, length) arrays (12 B per packet) are read but not in the algorithmic bytes"}
     # the packetizer: payload read in 256-B dword rows, wire written in 256-B dword rows — the shape
     # of membench's copy_rows (known bytes: 786432 x 4096 read, 786432 x 4152 written)
     cp = {k: v for k, v in mem.items() if k.startswith("copy_rows<0, 0>")}
@@ -115,6 +138,10 @@ def main():
             "traffic_bytes": round(fetch + write), "algorithmic_bytes": alg,
             "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
     print(json.dumps(res, indent=1))
+    for key, fname in (("icrc_traffic_per_launch", "pmc_traffic_c1.json"), ("c2_traffic_per_launch", "pmc_traffic_c2.json")):
+        if key in res:  # the records bench.py reads (copied to profiles/ as r05_pmc_traffic.json / r05_pmc_c2_traffic.json)
+            with open(os.path.join(out, fname), "w") as f:
+                json.dump(res[key], f, indent=1)
 
 
 if __name__ == "__main__":

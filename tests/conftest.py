@@ -39,15 +39,9 @@ def engine():
     e.close()
 
 
-# Kernel variants only the A/B library accepts (libicrc_amd_ab.so, built with ICRC_AB_BUILD): the
-# quad kernels (result-exact, kept for A/B) and their hybrid forms.  Diagnostics (wrong results by
-# design) are not listed: no parity test runs them.
-AB_ONLY_VARIANTS = {20, 24, 25, 26, 120, 124, 125, 126, 220, 224, 225, 226}
-
-
 @pytest.fixture(scope="session")
 def ab_engine():
-    """An engine of the A/B library (quad kernels + diagnostics), for the A/B variants' parity."""
+    """An engine of the A/B library (diagnostics), for the variant-validation test."""
     import icrc_amd
 
     if icrc_amd.device_count() <= 0:
@@ -56,6 +50,3 @@ def ab_engine():
     yield e
     e.close()
 
-
-def engine_for(variant, engine, ab_engine):
-    return ab_engine if variant in AB_ONLY_VARIANTS else engine

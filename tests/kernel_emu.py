@@ -194,7 +194,7 @@ def icrc(img: np.ndarray, pkt: np.ndarray) -> int:
     return int(~np.uint32(s) & 0xFFFFFFFF)
 
 
-# ---- quad kernel (icrc_quad.hip): four packets per wavefront, 16 lanes per packet ----------
+# ---- the oct kernel's per-packet path (group_slow_packet, icrc_device.h): W lanes per packet ----
 def _step_lanes(img, s, lanes):
     lo0 = (lanes & 31) * 4
     lo1 = lo0 + 128
@@ -205,9 +205,8 @@ def _step_lanes(img, s, lanes):
     return _lds(img, a0) ^ _lds(img, a1) ^ _lds(img, a2) ^ _lds(img, a3)
 
 
-def icrc_quad(img: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0, W: int = 16) -> int:
-    """One packet on lanes W*group .. W*group+W-1 of the quad (W = 16) or oct (W = 8) kernel, on
-    that kernel's table image: end-aligned rows of W stream words, `lead` extra leading zero
+def icrc_group(img: np.ndarray, pkt: np.ndarray, group: int = 0, lead: int = 0, W: int = 8) -> int:
+    """One packet on lanes W*group .. W*group+W-1 of the oct kernel (W = 8), on its table image: end-aligned rows of W stream words, `lead` extra leading zero
     rows (a shorter packet of a set runs behind the set's longest one), acc <- M^W(acc) ^ u,
     then XOR_c M^(W-c)(acc_c)."""
     Ld = pkt.size - 4

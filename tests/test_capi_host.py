@@ -28,9 +28,36 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 32, names
+    assert len(names) == 35, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
+
+
+def test_abi_version_and_struct_sizes():
+    """icrc_abi_check: the library's ABI version and the sizes of every struct a
+    binding mirrors; an 88-byte icrc_write_msg (the round-3 layout) or another version is refused."""
+    import icrc_amd
+
+    assert icrc_amd.lib.icrc_abi_version() == icrc_amd.ABI_VERSION == 5
+    assert icrc_amd.abi_check() == icrc_amd.OK
+    L = icrc_amd.lib
+    assert L.icrc_abi_check(5, 88, 72, 12, 40) == icrc_amd.EINVAL  # the round-3 icrc_write_msg
+    assert L.icrc_abi_check(4, 96, 72, 12, 40) == icrc_amd.EINVAL
+    assert L.icrc_abi_check(5, 96, 64, 12, 40) == icrc_amd.EINVAL
+    assert L.icrc_abi_check(5, 96, 72, 12, 40) == icrc_amd.OK
+
+
+@pytest.mark.parametrize("scenario,what", [(0, "normal"), (1, "device never completes: watchdog"),
+                                           (2, "launch ends mid-job: relaunch"), (3, "launch fails"),
+                                           (4, "idle exit before every call")])
+def test_submission_ring_protocol(scenario, what):
+    """The submission ring's host protocol (icrc_ring.cpp: slot allocation, publish order, per-wave
+    done words, relaunch of a launch that ended under a job, the 2 s-class watchdog that fails the
+    call with ICRC_ETIMEDOUT and retires the ring) from three threads against a simulated service
+    kernel on a CPU thread — the same code the GPU path runs, without a GPU."""
+    import icrc_amd
+
+    assert icrc_amd.ring_selftest(scenario, 3, 150) == 0, what
 
 
 def test_library_is_gfx950_hip_code():
@@ -145,9 +172,9 @@ def test_kernel_algorithm_emulation_matches_oracle(seed):
         assert kernel_emu.icrc(img, np.frombuffer(pkt, np.uint8)) == want
 
 
-@pytest.mark.parametrize("W", [16, 8])
-def test_quad_table_image_layout(W):
-    """Quad / oct images: M^W bulk tables, M^(W - (lane % W)) final tables, same addressing."""
+@pytest.mark.parametrize("W", [8])
+def test_oct_table_image_layout(W):
+    """The oct image: M^W bulk tables, M^(W - (lane % W)) final tables, same addressing."""
     import icrc_amd
 
     img = icrc_amd.table_image(width=W)
@@ -162,10 +189,10 @@ def test_quad_table_image_layout(W):
         assert img[addr // 4] == advance_words(v << (4 * n), W - (lane % W))
 
 
-@pytest.mark.parametrize("W", [16, 8])
+@pytest.mark.parametrize("W", [8])
 @pytest.mark.parametrize("seed", range(2))
-def test_quad_algorithm_emulation_matches_oracle(seed, W):
-    """The quad / oct kernels' lane algorithm (any packet group, leading zero rows of a shorter
+def test_group_algorithm_emulation_matches_oracle(seed, W):
+    """The oct kernel's per-packet lane algorithm (any packet group, leading zero rows of a shorter
     packet in a set) on the product's table image, against the oracle."""
     import icrc_amd
 
@@ -176,9 +203,9 @@ def test_quad_algorithm_emulation_matches_oracle(seed, W):
     for i, L in enumerate(lengths + [int(x) for x in rng.integers(44, 2000, 6)]):
         p = rng.integers(0, 256, L, dtype=np.uint8)
         want = oracle.compute_icrc(p)
-        assert kernel_emu.icrc_quad(img, p, group=i % G, lead=i % 3, W=W) == want, L
+        assert kernel_emu.icrc_group(img, p, group=i % G, lead=i % 3, W=W) == want, L
     for pkt, want in KATS:
-        assert kernel_emu.icrc_quad(img, np.frombuffer(pkt, np.uint8), group=G - 1, lead=2, W=W) == want
+        assert kernel_emu.icrc_group(img, np.frombuffer(pkt, np.uint8), group=G - 1, lead=2, W=W) == want
 
 
 @pytest.mark.parametrize("seed", range(2))
@@ -431,7 +458,7 @@ def test_header_is_c99_and_links(tmp_path):
     assert rc in (0, icrc_amd.ENODEV)  # ENODEV here (no GPU); 0 on a GPU box
 
 
-@pytest.mark.parametrize("W", [64, 16, 8])
+@pytest.mark.parametrize("W", [64, 8])
 def test_compact_table_replicates_to_the_lds_image(W):
     """The engine keeps a 36 KiB compact form after each 160 KiB image and every workgroup
     rebuilds the image in LDS from it (table_fill, icrc_device.h): thread t takes bulk entry t =

@@ -7,7 +7,6 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import AB_ONLY_VARIANTS, engine_for
 from golden_kats import KATS, KAT1, KAT1_ICRC
 
 torch = pytest.importorskip("torch")
@@ -87,11 +86,10 @@ def test_ragged_any_length_any_alignment(engine, seed):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
-@pytest.mark.parametrize("variant", [0, 13, 16, 17, 20, 24, 25, 26, 40])
-def test_every_kernel_variant_is_bit_exact(engine, ab_engine, variant):
+@pytest.mark.parametrize("variant", [0, 13, 16, 17, 40])
+def test_every_kernel_variant_is_bit_exact(engine, variant):
     """The A/B variants (unpipelined, S chains x D-deep prefetch) on a ragged batch with
     misaligned and over-long packets and on a strided stream."""
-    engine = engine_for(variant, engine, ab_engine)
     rng = np.random.default_rng(100 + variant)
     n = 1500
     lens = rng.choice([44, 48, 316, 1084, 4156, 4157, 5000, 9000], n).astype(np.uint32)
@@ -139,8 +137,8 @@ def test_every_kernel_variant_is_bit_exact(engine, ab_engine, variant):
         engine.set_variant(-1)
 
 
-def _quad_block_mix(rng, nblocks=48):
-    """Blocks of 64 packets of contrasting shapes for the quad kernel's block / set / bubble
+def _block_mix(rng, nblocks=48):
+    """Blocks of 64 packets of contrasting shapes for the oct kernel's block / set / frame
     logic: tiny 1-row packets (16 sets of 1 row per block: the load side outruns the process
     side and stalls), blocks with no fast-path packet at all (misaligned), partial sets, one
     jumbo packet among short ones, unsorted mixed MTUs."""
@@ -170,17 +168,16 @@ def _quad_block_mix(rng, nblocks=48):
     return off, lens
 
 
-@pytest.mark.parametrize("variant", [-1, 20, 24, 25, 26, 40, 120, 124, 140, 224, 240])
+@pytest.mark.parametrize("variant", [-1, 40, 140, 240])
 @pytest.mark.parametrize("n", [3072, 1000, 37])
-def test_quad_block_transitions_compute_verify(engine, ab_engine, variant, n):
-    """Quad (19-21) and oct (24-26) kernels and the hybrid dispatch (-1: oct for L < 2048, the
-    one-packet pipeline for the rest, or at these sizes the one-packet pipeline alone; 124 / 120: the
-    split forced, with oct / quad; 224: oct with the compacting long-packet walker) on contrasting 64-packet blocks: compute with trailer
+def test_block_transitions_compute_verify(engine, variant, n):
+    """The oct kernel (40) and the hybrid dispatch (-1: oct for L <= 1088, the one-packet pipeline
+    for the rest, or at these sizes the one-packet pipeline alone; 140: the split forced as two
+    kernels; 240: with the compacting long-packet walker) on contrasting 64-packet blocks: compute with trailer
     write, then verify (all ok), then negatives (one flipped bit per 7 packets) with in-place
     trailer zeroing."""
-    engine = engine_for(variant, engine, ab_engine)
     rng = np.random.default_rng((variant % 100 + 2) * 1000 + n)
-    off, lens = _quad_block_mix(rng)
+    off, lens = _block_mix(rng)
     off, lens = off[:n], lens[:n]
     buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
     engine.set_variant(variant)
@@ -1020,13 +1017,12 @@ def test_empty_batches_are_noops(engine):
     assert icrc_amd.compute_icrc_batch(np.zeros(0, np.uint8), [], []).size == 0
 
 
-@pytest.mark.parametrize("variant", [-1, 120, 124, 140])
+@pytest.mark.parametrize("variant", [-1, 40, 140])
 @pytest.mark.parametrize("pmtu", [256, 1024])
-def test_short_strided_stream_quad_path(engine, ab_engine, pmtu, variant):
+def test_short_strided_stream_oct_path(engine, pmtu, variant):
     """Uniform strided batches of short packets (at this size the one-packet pipeline by default;
-    forced to the quad (120) or oct (124) kernel, non-ragged variant): compute, trailer write and
-    verify against the oracle."""
-    engine = engine_for(variant, engine, ab_engine)
+    forced to the oct kernel, 40, or the forced split, 140): compute, trailer write and verify
+    against the oracle."""
     n = 2000 + pmtu // 256  # not a multiple of 4 or 64
     buf, off, lens = oracle.synth_middle_stream(n, pmtu=pmtu)
     L = int(lens[0])
@@ -1052,12 +1048,12 @@ def test_short_strided_stream_quad_path(engine, ab_engine, pmtu, variant):
     assert bool((d_ok == 1).all().item())
 
 
-@pytest.mark.parametrize("variant", [-1, 124, 140])
+@pytest.mark.parametrize("variant", [-1, 40, 140, 240])
 @pytest.mark.parametrize("n", [1, 2, 3, 5])
-def test_tiny_batches_every_path(engine, ab_engine, n, variant):
-    """1-5 packets: every wave but a few idle, sets of four partly empty, chunks below one block;
-    the default (one-packet pipeline at this size) and the split forced (124)."""
-    engine = engine_for(variant, engine, ab_engine)
+def test_tiny_batches_every_path(engine, n, variant):
+    """1-5 packets: every wave but a few idle, sets of eight partly empty, chunks below one block;
+    the default (one-packet pipeline at this size), the oct kernel (40) and the split forced (140,
+    240)."""
     rng = np.random.default_rng(900 + n)
     lens = rng.choice([44, 316, 1084, 4156, 9000], n).astype(np.uint32)
     off = np.zeros(n, np.uint64)
@@ -1152,24 +1148,29 @@ def test_split_batches_concurrent_streams(engine):
     assert not errors, errors
 
 
-DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 31, 32, 35, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 141, 146, 148, 241)
+DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 23, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 141, 146, 148, 241)
 
 
 def test_kernel_variant_validation(engine, ab_engine):
     """The product library accepts only result-exact variants; the diagnostics (wrong results by
-    design) and the quad kernels exist only in the A/B library (libicrc_amd_ab.so)."""
+    design) exist only in the A/B library (libicrc_amd_ab.so).  The retired quad kernels (20,
+    24-26, 31, 32, 35 and their hybrid forms) are refused by both."""
     import icrc_amd
 
     for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302):
         engine.set_variant(v)
     engine.set_variant(-1)
-    for v in (-2, 1, 10, 14, 23, 27, 36, 53, 99, 100, 116, 153, 303, 400) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
+    retired = (20, 24, 25, 26, 31, 32, 35, 120, 124, 220, 224)
+    for v in (-2, 1, 10, 14, 23, 27, 36, 53, 99, 100, 116, 153, 303, 400) + DIAGNOSTIC_VARIANTS + retired:
         with pytest.raises(icrc_amd.IcrcError) as e:
             engine.set_variant(v)
         assert e.value.rc == icrc_amd.EINVAL, v
-    for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302) + DIAGNOSTIC_VARIANTS + tuple(AB_ONLY_VARIANTS):
+    for v in (-1, 0, 13, 16, 17, 40, 140, 240, 301, 302) + DIAGNOSTIC_VARIANTS:
         ab_engine.set_variant(v)
     ab_engine.set_variant(-1)
+    for v in retired:
+        with pytest.raises(icrc_amd.IcrcError):
+            ab_engine.set_variant(v)
     assert "A/B build" in icrc_amd.ab_library().icrc_version().decode() and "A/B" not in icrc_amd.version()
 
 
@@ -1382,7 +1383,7 @@ def test_verify_residue_row_boundaries(engine, variant, zero_trailer):
         engine.set_variant(-1)
 
 
-def test_large_mixed_mtu_batch_oct_result_flushes(engine, ab_engine):
+def test_large_mixed_mtu_batch_oct_result_flushes(engine):
     """A C2-shaped batch big enough that every oct wave walks more than kOctRes (8) blocks, so its
     register-buffered block results are stored from inside the ring as well as after it: the
     default hybrid launch against the one-packet pipeline (forced variant 16) on every packet and
