@@ -907,15 +907,17 @@ def host_message_c0(eng, stream, args):
     out["c0_message_note"] = ("per message: icrc_compute_batch(write_trailer=1) + icrc_verify_batch(zero_trailer=1) on "
                               "a 64 x 4156-B WRITE in host memory; compare cpu_context.c0_roundtrip_1_core")
     # The same calls from native threads (scripts/_build/msg_probe, C++: the reference's callers are
-    # Rust threads; Python threads serialise on the GIL around every ctypes call), 1 and 3 threads.
+    # Rust threads; Python threads serialise on the GIL around every ctypes call), 1 and 3 threads:
+    # through the submission ring (the default host path) and one launch per call (ICRC_HOST_LAUNCH).
     probe = os.path.join(ROOT, "scripts", "_build", "msg_probe")
     if os.path.exists(probe):
-        env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(icrc_amd.LIB_PATH))
-        try:
-            r = subprocess.run([probe, "1000", "1", "3"], capture_output=True, text=True, timeout=180, env=env)
-            out["c0_message_native"] = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-        except (subprocess.TimeoutExpired, ValueError) as e:
-            out["c0_message_native"] = f"msg_probe failed: {e}"
+        for key, path in (("c0_message_native", "ring"), ("c0_message_native_launch", "launch")):
+            env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(icrc_amd.LIB_PATH), MSG_PROBE_PATH=path)
+            try:
+                r = subprocess.run([probe, "1000", "1", "3"], capture_output=True, text=True, timeout=180, env=env)
+                out[key] = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+            except (subprocess.TimeoutExpired, ValueError) as e:
+                out[key] = f"msg_probe failed: {e}"
     return out
 
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -687,9 +688,46 @@ int RingHip::ended() {
 // runtime's own teardown, which registered its handlers before ours.
 std::mutex g_ring_mu;
 std::vector<icrc::HostRing *> g_rings;
+#ifdef ICRC_AB_BUILD
+// ICRC_RING_TRACE (A/B library): per-slot job stamps from the ring kernel, summarised at exit
+struct RingTrace {
+    const uint64_t *rec;
+    uint32_t nslots;
+};
+std::vector<RingTrace> g_traces;
+void ring_trace_dump() {
+    for (const RingTrace &t : g_traces) {
+        std::vector<double> seen_dec, dec_res, res_done, gap;
+        for (uint32_t s = 0; s < t.nslots; ++s) {
+            const uint64_t *r = t.rec + static_cast<size_t>(s) * icrc::kRingTraceJobs * 4u;
+            for (uint32_t j = 1; j < icrc::kRingTraceJobs; ++j) {  // job numbers start at 1
+                const uint64_t *x = r + j * 4u;
+                if (!x[3]) continue;
+                seen_dec.push_back((x[1] - x[0]) * 0.01);
+                dec_res.push_back((x[2] - x[1]) * 0.01);
+                res_done.push_back((x[3] - x[2]) * 0.01);
+                if (j > 1 && x[-1] && x[0] > x[-1] && x[0] - x[-1] < 100000u) gap.push_back((x[0] - x[-1]) * 0.01);
+            }
+        }
+        auto med = [](std::vector<double> v) {
+            if (v.empty()) return 0.0;
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            return v[v.size() / 2];
+        };
+        std::fprintf(stderr,
+                     "{\"ring_trace\": true, \"jobs\": %zu, \"seen_to_decoded_us\": %.2f, \"decoded_to_results_us\": "
+                     "%.2f, \"results_to_done_us\": %.2f, \"done_to_next_seen_us\": %.2f}\n",
+                     seen_dec.size(), med(seen_dec), med(dec_res), med(res_done), med(gap));
+    }
+}
+#endif
+
 void ring_atexit() {
     std::lock_guard<std::mutex> lk(g_ring_mu);
     for (icrc::HostRing *r : g_rings) (void)r->stop(1000000);
+#ifdef ICRC_AB_BUILD
+    ring_trace_dump();
+#endif
 }
 
 void ring_free(icrc_engine *e) {
@@ -788,6 +826,22 @@ icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
     r->dev.rp.wg_per_slot = wgs;
     r->dev.rp.idle_ticks = kRingIdleTicks;
     r->dev.rp.life_ticks = kRingLifeTicks;
+    if (const char *v = std::getenv("ICRC_RING_LIFE_US"))  // measurement knob: 100 us .. 20 ms
+        r->dev.rp.life_ticks = static_cast<uint32_t>(std::max(100, std::min(20000, std::atoi(v))) * 100);
+#ifdef ICRC_AB_BUILD
+    if (const char *v = std::getenv("ICRC_RING_AB")) r->dev.rp.ab = static_cast<uint32_t>(std::atoi(v));
+    if (std::getenv("ICRC_RING_TRACE")) {  // never freed: read at exit
+        void *tp = nullptr, *tdv = nullptr;
+        const size_t tb = static_cast<size_t>(nslots) * icrc::kRingTraceJobs * 32u;
+        if (hipHostMalloc(&tp, tb, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer(&tdv, tp, 0) == hipSuccess) {
+            std::memset(tp, 0, tb);
+            r->dev.rp.trace = static_cast<uint64_t *>(tdv);
+            std::lock_guard<std::mutex> gl(g_ring_mu);
+            g_traces.push_back({static_cast<const uint64_t *>(tp), nslots});
+        }
+    }
+#endif
     r->ring = std::make_unique<icrc::HostRing>(&r->dev, mem, nslots, wgs, kRingWatchdogUs);
     {
         static std::once_flag once;

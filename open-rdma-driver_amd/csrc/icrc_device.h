@@ -245,10 +245,15 @@ __device__ __forceinline__ uint32_t handle_packet(const BatchParams &p, uint8_t 
     return packet_result<MODE>(p, pkt, Ld, ~wave_xor(final_mul(lds, acc, c.fin)), fast, lane);
 }
 
-template <int MODE>
+// SYS: a system-scope store (written through to host memory, complete once acknowledged) — the
+// ring's results, which the host reads as soon as the job's done word arrives.
+template <int MODE, bool SYS = false>
 __device__ __forceinline__ void store_result(const BatchParams &p, uint32_t i, uint32_t r) {
     if (MODE == kCompute) {
-        if (p.out) p.out[i] = r;
+        if (SYS && p.out)
+            __hip_atomic_store(p.out + i, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (p.out)
+            p.out[i] = r;
     } else {
         if (p.ok) p.ok[i] = static_cast<uint8_t>(r);
     }
@@ -266,9 +271,9 @@ __device__ __forceinline__ void rb_put(ResultBuf &rb, uint32_t q, uint32_t r) {
     rb.valid |= 1ull << (q & 63u);
 }
 
-template <int MODE>
+template <int MODE, bool SYS = false>
 __device__ __forceinline__ void rb_flush(const BatchParams &p, ResultBuf &rb, uint32_t base, uint32_t lane) {
-    if ((rb.valid >> lane) & 1ull) store_result<MODE>(p, base + lane, rb.v);
+    if ((rb.valid >> lane) & 1ull) store_result<MODE, SYS>(p, base + lane, rb.v);
     rb.valid = 0;
 }
 

@@ -165,7 +165,8 @@ constexpr uint32_t kRingStop = 0x80000000u;  // RingSlot::cmd: every wave exits
 constexpr uint32_t kRingMaxPackets = 1024u;  // packets per job (one message)
 constexpr uint32_t kRingMaxSlots = 16u;
 constexpr uint32_t kRingSlots = 4u;          // default: one per emulator thread (3) + one
-constexpr uint32_t kRingWgPerSlot = 8u;      // default workgroups per slot (CUs reading one message)
+constexpr uint32_t kRingWgPerSlot = 2u;      // default workgroups per slot (CUs reading one message):
+                                             // 2 beat 4 and 8 from 3-4 threads (profiles/r05/ring/)
 struct alignas(64) RingSlot {  // host-written, one 64-byte line per slot
     uint32_t cmd;       // job number (bits 0-30, never 0 for a job) | kRingStop; written last
     uint32_t activity;  // the host's submission counter, copied into every slot on every call
@@ -176,9 +177,28 @@ struct alignas(64) RingSlot {  // host-written, one 64-byte line per slot
     uint64_t off;       // device address of n u64 offsets from base (ulen == 0)
     uint64_t len;       // device address of n u32 lengths (ulen == 0)
     uint64_t out;       // device address of n u32 ICRCs (coherent mapped host memory)
-    uint32_t rsvd[2];
+    uint32_t reserved;  // 0
+    uint32_t hash;      // ring_line_hash of the line, written before cmd: the kernel reads the line in
+                        // one load per poll and takes its fields only when the hash matches (a read
+                        // torn by the host's writes is read again)
 };
 static_assert(sizeof(RingSlot) == 64, "one line per slot");
+#ifdef __HIPCC__
+#define ICRC_HD __host__ __device__
+#else
+#define ICRC_HD
+#endif
+// Hash of a slot line's dwords 0 (cmd) and 2..14 (the job), kept in dword 15.
+ICRC_HD inline uint32_t ring_line_hash(uint32_t h, uint32_t d) {
+    h ^= d;
+    h *= 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+ICRC_HD inline uint32_t ring_line_hash(const uint32_t *w) {
+    uint32_t h = ring_line_hash(0x9E3779B9u, w[0]);
+    for (int k = 2; k < 15; ++k) h = ring_line_hash(h, w[k]);
+    return h;
+}
 struct RingParams {
     const RingSlot *slots;  // device view of the slot lines (host memory)
     uint32_t *done;         // [slot][wg]: the last cmd each workgroup finished (host memory)
@@ -192,7 +212,13 @@ struct RingParams {
     uint32_t life_ticks;    // ... and since the launch: a launch ends at a job boundary after this long,
                             // so a kernel that needs every CU (the batch kernels: one 160 KiB workgroup
                             // per CU) waits at most that long for the CUs the ring holds
+    uint32_t ab;            // A/B library only (ICRC_RING_AB, diagnostic cuts): 1 no acquire, 2 a
+                            // release fence after the results, 4 no sleep between polls, 8 no compute; 0 in the product
+    uint64_t *trace;        // A/B library only (ICRC_RING_TRACE): per slot, kRingTraceJobs records of
+                            // s_memrealtime stamps {cmd seen, job decoded, results complete, done
+                            // stored} by the slot's first workgroup; nullptr in the product
 };
+constexpr uint32_t kRingTraceJobs = 4096;
 int launch_ring(const RingParams &rp, uint32_t nslots, void *stream);
 
 // Segmentation shared by host and tests (generate_segments_from_request, common.rs:152-176).

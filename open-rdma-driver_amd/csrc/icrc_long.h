@@ -117,6 +117,13 @@ struct Ring {
     // profiles/r04_ab_ragged_scalar_meta.jsonl).  The batch kernel keeps the vector blocks: its
     // small batches (a wave per packet) wait longer for a scalar load.
     static constexpr bool kScalarMeta = true;
+    static constexpr bool kSysStores = false;  // results by system-scope stores (RingHostResults)
+};
+// The submission ring's jobs (icrc_ring_kernel.hip): results written through to host memory, so the
+// job needs no L2 write-back before its done word (a system-scope release fence cost ~4 us per
+// 64-packet job, scripts/gpu_r05_ring_ab.sh).
+struct RingHostResults : Ring<kStreamAux> {
+    static constexpr bool kSysStores = true;
 };
 #ifdef ICRC_AB_BUILD
 // (A/B, ICRC_AB_LONG_VMETA=1: the hybrid's dense long walk) the default ring with the (offset,
@@ -667,8 +674,8 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
                 if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + ((q0 >> 6) << 6), rb.v, lane);
                 // !A::kStores (A/B): only the chunk's last block is stored (its lanes depend on every
                 // earlier packet through rb_put's selects, so nothing is dead code)
-                if constexpr (A::kStores) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
-                else if (qn >= nq) rb_flush<MODE>(p, rb, lo + ((q0 >> 6) << 6), lane);
+                if constexpr (A::kStores) rb_flush<MODE, A::kSysStores>(p, rb, lo + ((q0 >> 6) << 6), lane);
+                else if (qn >= nq) rb_flush<MODE, A::kSysStores>(p, rb, lo + ((q0 >> 6) << 6), lane);
             }
             return true;
         });

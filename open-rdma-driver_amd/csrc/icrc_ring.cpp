@@ -100,16 +100,24 @@ int HostRing::submit(const RingJob &j) {
         std::memcpy(mem_.off[s], j.off, j.n * sizeof(uint64_t));
         std::memcpy(mem_.len[s], j.len, j.n * sizeof(uint32_t));
     }
-    S->n = j.n;
-    S->ulen = j.ulen;
-    S->base = j.dbase;
-    S->stride = j.stride;
-    S->off = mem_.d_off[s];
-    S->len = mem_.d_len[s];
-    S->out = mem_.d_res[s];
     uint32_t cmd = (seq_[s] + 1u) & ~kRingStop;
     if (cmd == 0u) cmd = 1u;
     seq_[s] = cmd;
+    RingSlot line;  // the new line: fields, hash (over cmd too), then in memory: fields, hash, cmd
+    std::memset(&line, 0, sizeof line);
+    line.cmd = cmd;
+    line.n = j.n;
+    line.ulen = j.ulen;
+    line.base = j.dbase;
+    line.stride = j.stride;
+    line.off = mem_.d_off[s];
+    line.len = mem_.d_len[s];
+    line.out = mem_.d_res[s];
+    line.reserved = 0u;
+    line.hash = ring_line_hash(reinterpret_cast<const uint32_t *>(&line));
+    uint32_t *w = reinterpret_cast<uint32_t *>(S);
+    const uint32_t *nw = reinterpret_cast<const uint32_t *>(&line);
+    for (int k = 2; k < 16; ++k) __atomic_store_n(w + k, nw[k], __ATOMIC_RELAXED);
     const uint32_t act = activity_.fetch_add(1u, std::memory_order_relaxed) + 1u;
     for (uint32_t k = 0; k < nslots_; ++k) __atomic_store_n(&mem_.slots[k].activity, act, __ATOMIC_RELAXED);
     __atomic_store_n(&S->cmd, cmd, __ATOMIC_RELEASE);  // publishes the fields above (x86: ordered stores)
@@ -249,6 +257,9 @@ struct SimDevice final : RingDevice {
                     if (cmd == last[static_cast<size_t>(s) * wps] && cmd == last[static_cast<size_t>(s) * wps + wps - 1]) continue;
                     any = true;
                     const RingSlot &S = mem.slots[s];
+                    uint32_t line[16];  // what the kernel checks before it takes the fields
+                    for (int k = 0; k < 16; ++k) line[k] = __atomic_load_n(reinterpret_cast<const uint32_t *>(&S) + k, __ATOMIC_ACQUIRE);
+                    if (line[0] != cmd || ring_line_hash(line) != line[15]) continue;  // torn: read again
                     if (scenario == 1) continue;  // never completes
                     const uint32_t job = ++jobs_seen;
                     const uint32_t chunk = (S.n + wps - 1u) / wps;

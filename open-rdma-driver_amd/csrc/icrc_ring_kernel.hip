@@ -13,15 +13,18 @@ namespace {
 
 // ---- host-message service kernel (the submission ring, icrc_internal.h / icrc_ring.cpp) -----------
 // Workgroup b serves slot b / wg_per_slot.  While idle only wave 0 of each workgroup runs (the others
-// wait at a barrier): it polls the slot's line in coherent host memory.  On a new cmd it reads the
-// whole line again (one load per lane: the fields the host wrote before cmd) and copies it into the
-// workgroup's decision line in device memory; every wave reads that line after a barrier, so all of
-// them take the same branch (the host line may change meanwhile: a stop bit).  The workgroup's waves
-// take contiguous chunks of its share on the one-packet pipeline — its row loads system-coherent
-// (sc0 sc1: the caller may have rewritten its packets since an earlier job read them, trailers or a
-// new message in the same buffer, and no cached line of host memory may answer) — results straight
-// into the slot's coherent result array; after a system-scope release and a second barrier wave 0
-// stores the cmd in the workgroup's done word.
+// wait at a barrier): it polls the slot's 64-byte line in coherent host memory, the whole line in one
+// load (dword k in lane k).  On a new cmd whose line hash matches (ring_line_hash: a read torn by
+// the host's writes is simply read again) it copies the line into the workgroup's decision line in
+// device memory and invalidates this CU's and this XCD's cached lines of host memory (a system-scope
+// acquire: the caller may have rewritten its packets since an earlier job read them, trailers or a new
+// message in the same buffer, and the slot's offset / length arrays are rewritten every job; loads
+// with sc0 sc1 alone were measured to return such a stale line, and so did skipping the acquire for
+// coherent host memory — hipHostMallocCoherent lines are cached too).  Every wave reads the decision
+// line after a barrier, so all of them take the same branch (the host line may change meanwhile: a
+// stop bit).  The workgroup's waves take contiguous chunks of its share on the one-packet pipeline,
+// results straight into the slot's coherent result array by system-scope stores; once every wave's
+// stores have completed (s_waitcnt, then a barrier) wave 0 stores the cmd in the workgroup's done word.
 // The end: kRingStop in the slot, or the exit flag, which the slot's leader (wave 0 of its first
 // workgroup) sets when the host has made no call (RingSlot::activity) for idle_ticks or the launch
 // has run for life_ticks (a persistent launch must not hold its CUs from other kernels for long:
@@ -51,8 +54,6 @@ __device__ __forceinline__ uint32_t line_load_dev(const RingSlot *line, uint32_t
 __device__ __forceinline__ uint64_t line_u64(uint32_t v, int dword) {
     return static_cast<uint64_t>(readlane_u32(v, dword)) | (static_cast<uint64_t>(readlane_u32(v, dword + 1)) << 32);
 }
-// The ring's row loads: system-coherent, read-once (sc0 nt sc1).
-constexpr int kRingRowAux = 0x13;
 
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams rp) {
     __shared__ uint4 lds4[kLdsBytes / 16];
@@ -73,45 +74,53 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams 
     uint32_t act = 0u;
     uint64_t t_act = 0, t_launch = 0;
     if (leader) {
-        act = __builtin_amdgcn_readfirstlane(sys_load(&S->activity));
+        act = readlane_u32(line_load_sys(S, lane), 1);
         t_act = t_launch = __builtin_amdgcn_s_memrealtime();
     }
     const uint64_t max_polls = 8ull * rp.idle_ticks + 4096u;  // a poll takes well over 1 tick
+    uint64_t *tr = (rp.trace && sub == 0u && wave == 0u) ? rp.trace + slot * kRingTraceJobs * 4u : nullptr;
+    uint64_t t_seen = 0;
     for (;;) {
         if (wave == 0u) {
             uint32_t dec = kRingStop;
-            for (uint64_t polls = 0; polls < max_polls; ++polls) {
-                if (dev_load(rp.exit_flag) == rp.epoch) break;
-                const uint32_t cmd = __builtin_amdgcn_readfirstlane(sys_load(&S->cmd));
-                if (cmd & kRingStop) break;
+            // Is this poll's (exit flag, line) the end of the wait?  dec is set when it is a job.
+            auto look = [&](uint32_t efv, uint32_t v) __attribute__((always_inline)) -> bool {
+                if (__builtin_amdgcn_readfirstlane(efv) == rp.epoch) return true;
+                const uint32_t cmd = readlane_u32(v, 0);
+                if (cmd & kRingStop) return true;
                 if (cmd != last) {
-                    // the host wrote the fields, then cmd: read the line again after cmd has arrived
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    const uint32_t v = line_load_sys(S, lane);
+                    uint32_t h = ring_line_hash(0x9E3779B9u, cmd);
+                    for (int k = 2; k < 15; ++k) h = ring_line_hash(h, readlane_u32(v, k));
+                    if (h != readlane_u32(v, 15)) return false;  // a torn line: read it again
                     if (lane >= 1u && lane < 16u)  // dword 0 (cmd) last, below
                         __hip_atomic_store(reinterpret_cast<uint32_t *>(D) + lane, v, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+                    if (!(rp.ab & 1u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // stale host-memory lines out
                     dec = cmd;
-                    break;
+                    if (tr) t_seen = __builtin_amdgcn_s_memrealtime();
+                    return true;
                 }
                 if (leader) {
-                    const uint32_t a = __builtin_amdgcn_readfirstlane(sys_load(&S->activity));
+                    const uint32_t a = readlane_u32(v, 1);
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (a != act) {
                         act = a;
                         t_act = now;
-                    } else if (now - t_act > rp.idle_ticks || now - t_launch > rp.life_ticks) {
-                        dev_store(rp.exit_flag, rp.epoch);  // idle, or the launch's time is up
-                        break;
                     }
-                    if (now - t_launch > rp.life_ticks) {  // time up while calls keep coming
-                        dev_store(rp.exit_flag, rp.epoch);
-                        break;
-                    }
+                    // idle, or the launch's time is up (also while calls keep coming)
+                    if (now - t_act > rp.idle_ticks || now - t_launch > rp.life_ticks) return true;
                 }
-                __builtin_amdgcn_s_sleep(2);
-                if (polls + 1u == max_polls) dev_store(rp.exit_flag, rp.epoch);
+                if (!(rp.ab & 4u)) __builtin_amdgcn_s_sleep(2);
+                return false;
+            };
+            // one poll at a time: two in flight (the next loads issued before this pair is looked at)
+            // compiled to a full wait at the loop head anyway
+            for (uint64_t polls = 0; polls < max_polls; ++polls) {
+                const uint32_t efv = __hip_atomic_load(rp.exit_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (look(efv, line_load_sys(S, lane))) break;  // the whole line: dword k in lane k
             }
+            // no job (stop bit, exit flag, idle, lifetime or the poll cap): the whole launch ends
+            if (dec == kRingStop) dev_store(rp.exit_flag, rp.epoch);
             dev_store(&D->cmd, dec);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -119,6 +128,7 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams 
         const uint32_t dl = line_load_dev(D, lane);  // RingSlot dwords: 0 cmd, 2 n, 3 ulen, 4-5 base, 6-7 stride,
         const uint32_t cmd = readlane_u32(dl, 0);     // 8-9 off, 10-11 len, 12-13 out
         if (cmd & kRingStop) break;
+        const uint64_t t_dec = tr ? __builtin_amdgcn_s_memrealtime() : 0u;
         const uint32_t n = readlane_u32(dl, 2);
         BatchParams p{};
         p.n = n;
@@ -132,20 +142,28 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams 
         p.out = reinterpret_cast<uint32_t *>(line_u64(dl, 12));
         p.table = rp.table;
         p.skew = 0u;
-        if (n <= kRingMaxPackets) {  // the host never posts more; a corrupt line does nothing
+        if (n <= kRingMaxPackets && !(rp.ab & 8u)) {  // the host never posts more; a corrupt line does nothing
             const uint32_t nwaves = rp.wg_per_slot * kWavesPerGroup;
             const uint32_t chunk = (n + nwaves - 1u) / nwaves;
             const uint32_t w = sub * kWavesPerGroup + wave;
             const uint32_t lo = w * chunk < n ? w * chunk : n;
             const uint32_t nq = (n - lo) < chunk ? (n - lo) : chunk;
-            run_pipelined<kCompute, 2, 1, Ring<kRingRowAux>>(p, lds, c, lane, lo, nq);
+            run_pipelined<kCompute, 2, 1, RingHostResults>(p, lds, c, lane, lo, nq);
         }
-        // the results, then (every wave past the barrier) the done word: the release recipe of the
-        // guide (fence, an explicit wait the compiler cannot drop, then the flag)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // the results (system-scope stores: written through, complete once acknowledged — plain
+        // stores without a release fence were measured to reach the host after the done word), then
+        // (every wave past the barrier) the done word; an explicit wait the compiler cannot drop
+        if (rp.ab & 2u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // A/B: the fence as well
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // also: every wave has read the decision before wave 0 rewrites it
+        const uint64_t t_res = tr ? __builtin_amdgcn_s_memrealtime() : 0u;
         if (wave == 0u && lane == 0u) sys_store(rp.done + widx, cmd);
+        if (tr) {  // A/B trace (ICRC_RING_TRACE), record (job number % kRingTraceJobs): the done store's completion too
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t t_done = __builtin_amdgcn_s_memrealtime();
+            const uint32_t tj = cmd % kRingTraceJobs;
+            if (lane < 4u) tr[tj * 4u + lane] = lane == 0u ? t_seen : lane == 1u ? t_dec : lane == 2u ? t_res : t_done;
+        }
         last = cmd;
     }
     if (wave == 0u) {

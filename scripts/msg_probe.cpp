@@ -10,6 +10,7 @@
 // (the default); the last line is the ring's counters (icrc_engine_host_stats).
 // Build: see scripts/Makefile (links libicrc_amd.so and the HIP runtime for pinned memory).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -62,15 +63,29 @@ void run(const char *name, uint8_t *buf, uint32_t npk, uint32_t L, int calls) {
     fflush(stdout);
 }
 
-// T threads, each its own pinned (or pageable) copy of the message, each running `calls` messages
+// T threads, each its own pinned (kind 1; kind 2: pinned and coherent; kind 3: 2 MiB transparent huge
+// pages registered with hipHostRegister) or pageable (kind 0) copy of the message, each running `calls` messages
 // (compute + verify): messages/s in total and p50 / p99 per message — the emulator's three callers.
-void run_threads(const char *name, const std::vector<uint8_t> &src, bool pinned_bufs, uint32_t npk, uint32_t L,
+void run_threads(const char *name, const std::vector<uint8_t> &src, int kind, uint32_t npk, uint32_t L,
                  int calls, int T) {
+    const bool pinned_bufs = kind != 0;
     std::vector<uint8_t *> bufs(T);
     std::vector<std::vector<uint8_t>> pageable(T);
     for (int t = 0; t < T; ++t) {
-        if (pinned_bufs) {
-            if (hipHostMalloc(reinterpret_cast<void **>(&bufs[t]), src.size(), hipHostMallocDefault) != hipSuccess) {
+        if (kind == 3) {
+            const size_t hb = (src.size() + (2u << 20) - 1) & ~((size_t(2) << 20) - 1);
+            void *m = nullptr;
+            if (posix_memalign(&m, size_t(2) << 20, hb) != 0) exit(1);
+            (void)madvise(m, hb, MADV_HUGEPAGE);
+            std::memset(m, 0, hb);
+            if (hipHostRegister(m, hb, hipHostRegisterMapped) != hipSuccess) {
+                fprintf(stderr, "hipHostRegister failed\n");
+                exit(1);
+            }
+            bufs[t] = static_cast<uint8_t *>(m);
+        } else if (pinned_bufs) {
+            const unsigned fl = kind == 2 ? hipHostMallocCoherent : hipHostMallocDefault;
+            if (hipHostMalloc(reinterpret_cast<void **>(&bufs[t]), src.size(), fl) != hipSuccess) {
                 fprintf(stderr, "hipHostMalloc failed\n");
                 exit(1);
             }
@@ -120,8 +135,14 @@ void run_threads(const char *name, const std::vector<uint8_t> &src, bool pinned_
            "\"message_p50_us\": %.1f, \"message_p99_us\": %.1f, \"bad\": %ld}\n",
            name, T, npk, L, T * calls / secs, pct(all, 0.5), pct(all, 0.99), bad.load());
     fflush(stdout);
-    if (pinned_bufs)
+    if (kind == 3) {
+        for (auto *b : bufs) {
+            (void)hipHostUnregister(b);
+            free(b);
+        }
+    } else if (pinned_bufs) {
         for (auto *b : bufs) (void)hipHostFree(b);
+    }
 }
 
 }  // namespace
@@ -168,8 +189,10 @@ int main(int argc, char **argv) {
     if (argc > 2) {  // msg_probe CALLS THREADS...: the multi-threaded message rate only
         for (int a = 2; a < argc; ++a) {
             const int T = atoi(argv[a]);
-            run_threads(launch ? "pinned, launch" : "pinned, ring", pageable, true, npk, L, calls, T);
-            run_threads(launch ? "pageable, launch" : "pageable, ring", pageable, false, npk, L, calls, T);
+            run_threads(launch ? "pinned, launch" : "pinned, ring", pageable, 1, npk, L, calls, T);
+            run_threads(launch ? "pinned_coherent, launch" : "pinned_coherent, ring", pageable, 2, npk, L, calls, T);
+            run_threads(launch ? "registered_huge, launch" : "registered_huge, ring", pageable, 3, npk, L, calls, T);
+            run_threads(launch ? "pageable, launch" : "pageable, ring", pageable, 0, npk, L, calls, T);
         }
         print_stats(path);
         (void)hipHostFree(pinned);
