@@ -78,8 +78,9 @@ def parse(argv=None):
                     help="per rank: packets at each end of the shard checked against the CPU restatement")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the configs[2] / configs[3] legs of the default line (N = 1)")
-    ap.add_argument("--c2-only", action="store_true",
-                    help="time only the configs[2] kernel and print its leg (rocprofv3 --pmc passes)")
+    ap.add_argument("--only", choices=("c2", "rx", "msg"), default=None,
+                    help="run one secondary leg alone and print it: c2 = the configs[2] kernel (rocprofv3 --pmc "
+                         "passes), rx = the short-packet / configs[2] receive legs, msg = the per-message host legs")
     ap.add_argument("--extra", action="store_true",
                     help="also time verify, trailer stores, mixed-MTU, 16 MiB round trip, packetizer, receive "
                          "parse and the host-resident path")
@@ -261,12 +262,20 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         log(f"bench.py: rank {rank}: engine on device {eng.ordinal}, expected LOCAL_RANK {local}")
         return 2
     stream = torch.cuda.current_stream().cuda_stream
-    if args.c2_only:
+    if args.only == "c2":
         import oracle as orc
 
         leg, fails = config_c2(eng, stream, args, world, orc)
         print(json.dumps({"configs": {"c2": leg}}), flush=True)
         return 1 if fails else 0
+    if args.only == "rx":
+        rx = receive_short(eng, stream, args, world)
+        print(json.dumps(rx), flush=True)
+        return 0 if all(v["all_ok"] for v in rx.values()) else 1
+    if args.only == "msg":
+        msg = host_message_c0(eng, stream, args)
+        print(json.dumps(msg), flush=True)
+        return 0
 
     # ---- C1 workload: weak = one QP stream per rank; strong = a shard of one stream ----
     if args.scaling == "weak":
@@ -720,6 +729,7 @@ def extra_measurements(eng, stream, args, world):
     del d_buf, d_off, d_len, d_out, d_ok
 
     ex.update(fused_send_receive(eng, stream, args, world))
+    ex.update(receive_short(eng, stream, args, world))
     ex.update(host_resident(eng, stream, args))
     ex.update(host_message_c0(eng, stream, args))
     return ex
@@ -801,6 +811,53 @@ def fused_send_receive(eng, stream, args, world):
     return out
 
 
+def receive_short(eng, stream, args, world):
+    """§8f row 3 at the emulator's receive shapes: icrc_rx_parse_device (verify + strip + parse)
+    over configs[2]'s mixed-MTU batch with its trailers written (`rx_verify_parse_c2`), and over 4 Mi
+    316-byte packets (the 256-B MTU class) as a ragged batch and as a strided one.  Algorithmic HBM
+    bytes per packet: the packet read + a 72-byte descriptor + an ok byte written."""
+    import torch
+
+    import icrc_amd
+    from icrc_amd import workloads
+
+    out = {}
+    desc_b = icrc_amd.RX_DESC_DTYPE.itemsize
+
+    def leg(w, ragged):
+        d_buf = workloads.synthesize(eng, w, stream=stream)
+        d_off, d_len = dev(w.off), dev(w.lens)
+        d_tmp = torch.zeros(w.n, dtype=torch.int32, device="cuda")
+        eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_tmp.data_ptr(), True, 0, stream)
+        torch.cuda.synchronize()
+        del d_tmp
+        d_desc = torch.empty(w.n * desc_b, dtype=torch.uint8, device="cuda")
+        d_ok = torch.zeros(w.n, dtype=torch.uint8, device="cuda")
+        L = int(w.lens[0])
+        if ragged:
+            fn = lambda: eng.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_desc.data_ptr(),
+                                      d_ok.data_ptr(), stream=stream)
+        else:
+            fn = lambda: eng.rx_parse(d_buf.data_ptr(), 0, 0, w.n, d_desc.data_ptr(), d_ok.data_ptr(),
+                                      stride=L, length=L, stream=stream)
+        _, kms = time_kernel(fn, min(args.steps, 20), min(args.warmup, 5), world)
+        tot = int(w.lens.astype(np.uint64).sum())
+        alg = tot + w.n * (desc_b + 1)
+        desc = d_desc[: 64 * desc_b].cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+        res = {"packets": w.n, "packet_bytes": tot, "kernel_ms": round(kms, 4),
+               "hbm_GB/s": round(alg / (kms * 1e-3) / 1e9, 1), "frac_of_peak": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "all_ok": bool((d_ok == 1).all().item()), "first_desc_payload_len": int(desc["payload_len"][0])}
+        del d_buf, d_off, d_len, d_desc, d_ok
+        torch.cuda.empty_cache()
+        return res
+
+    out["rx_verify_parse_c2"] = leg(workloads.mixed_mtu_stream(4 << 20), True)
+    w316 = workloads.write_middle_stream(4 << 20, 256)
+    out["rx_verify_parse_316_ragged"] = leg(w316, True)
+    out["rx_verify_parse_316_strided"] = leg(w316, False)
+    return out
+
+
 def host_resident(eng, stream, args):
     """Packets in host memory (pinned and pageable) -> H2D -> kernel -> ICRCs back (PCIe bound;
     never the headline value)."""
@@ -861,7 +918,7 @@ def host_message_c0(eng, stream, args):
     src = d_buf.cpu().numpy()
     off, lens = np.ascontiguousarray(w.off, np.uint64), np.ascontiguousarray(w.lens, np.uint32)
     nbytes = int(lens.astype(np.uint64).sum())
-    reps = max(200, args.steps * 4)
+    reps = max(1000, args.steps * 4)
     out = {}
     for kind in ("pinned", "pageable"):
         for nth in (1, 3):
@@ -876,33 +933,40 @@ def host_message_c0(eng, stream, args):
                     bufs.append((None, src.copy()))
             lat = [[] for _ in range(nth)]
             bad = [0] * nth
-            gate = threading.Barrier(nth)
+            ends = [0.0] * nth
+            start = [0.0]
+            # warm-up calls (first touch of the buffer, the ring's launch) outside the timed region:
+            # every thread warms, then all are released together; messages/s = the timed messages
+            # over (last thread's end - release).  (Round 4 counted thread start and the warm-up
+            # calls in the rate: the 1-thread pinned case, first in the sequence, read half its p50.)
+            gate = threading.Barrier(nth, action=lambda: start.__setitem__(0, time.perf_counter()))
 
             def worker(k):
                 b = bufs[k][1]
-                for i in range(reps + 10):
-                    if i == 0:
+                for i in range(reps + 20):
+                    if i == 20:
                         gate.wait()
                     t0 = time.perf_counter_ns()
                     icrc_amd.compute_icrc_batch(b, off, lens, write_trailer=True)
                     ok = icrc_amd.verify_icrc_batch(b, off, lens, zero_trailer=True)
                     t1 = time.perf_counter_ns()
-                    if i >= 10:  # warm
+                    if i >= 20:
                         lat[k].append((t1 - t0) / 1e3)
                     bad[k] += int(np.count_nonzero(ok != 1))
+                ends[k] = time.perf_counter()
 
             ths = [threading.Thread(target=worker, args=(k,)) for k in range(nth)]
-            t0 = time.perf_counter()
             for th in ths:
                 th.start()
             for th in ths:
                 th.join()
-            secs = time.perf_counter() - t0
+            secs = max(ends) - start[0]
             allv = np.concatenate([np.asarray(x) for x in lat])
             out[f"c0_message_{kind}_{nth}_thread"] = {
                 "p50_us": round(float(np.percentile(allv, 50)), 1), "p99_us": round(float(np.percentile(allv, 99)), 1),
-                "messages_per_s": round(nth * (reps + 10) / secs, 1),
-                "GiB/s": round(nth * (reps + 10) * nbytes / secs / GIB, 3),
+                "mean_us": round(float(np.mean(allv)), 1),
+                "messages_per_s": round(nth * reps / secs, 1),
+                "GiB/s": round(nth * reps * nbytes / secs / GIB, 3),
                 "failed_verifies": int(sum(bad)), "packets_per_message": int(w.n), "message_bytes": nbytes}
     out["c0_message_note"] = ("per message: icrc_compute_batch(write_trailer=1) + icrc_verify_batch(zero_trailer=1) on "
                               "a 64 x 4156-B WRITE in host memory; compare cpu_context.c0_roundtrip_1_core")

@@ -25,7 +25,7 @@ for path in sorted(glob.glob(f"gpurun_out/pmclds_{W}_*/**/*counter_collection.cs
         k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("icrc::", "").split("(icrc::BatchParams")[0].split("(BatchParams")[0][:72]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     for k, d in acc.items():
-        if any(t in k for t in ("icrc_oct", "icrc_batch", "icrc_quad", "icrc_long")):
+        if any(t in k for t in ("icrc_oct", "icrc_batch", "icrc_hybrid", "icrc_long")):
             print(k, {c: f"{v:.4g}" for c, v in sorted(d.items())})
 PY
 echo "== done"
