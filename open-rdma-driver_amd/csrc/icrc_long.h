@@ -834,14 +834,18 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     const uint32_t chunk = wave_chunk(p.n, tw);
     const uint64_t g0 = static_cast<uint64_t>(bid) * kWavesPerGroup * chunk;
     // The waves' shares: skewed by age as in the batch kernel (p.skew's long half) when the
-    // workgroup's range is dense with long packets (its first 64, the same sample in every wave),
-    // equal otherwise — on sparse ranges (C2) a skew measured slower
-    // (profiles/r03_probe_skew_long.jsonl; dense: profiles/r04_ab_long_dense_skew.jsonl).
+    // workgroup's range is dense with long packets, equal otherwise — on sparse ranges (C2) a skew
+    // measured slower (profiles/r03_probe_skew_long.jsonl; dense: profiles/r04_ab_long_dense_skew.jsonl).
+    // The sample: 64 lengths spread evenly over the whole range (the same in every wave), so a range
+    // that turns sparse after its first packets does not take the dense range's skew.
     uint32_t skew = 0u;
     if (!COMPACT && p.len != nullptr && g0 < p.n) {
-        const uint64_t i = g0 + lane;
-        const uint64_t dm = __ballot(i < p.n && p.len[i] >= p.split_len);
-        const uint32_t ns = p.n - g0 < 64u ? static_cast<uint32_t>(p.n - g0) : 64u;
+        const uint64_t span = (p.n - g0 < static_cast<uint64_t>(kWavesPerGroup) * chunk)
+                                  ? p.n - g0 : static_cast<uint64_t>(kWavesPerGroup) * chunk;
+        const uint64_t step = span > 64u ? span / 64u : 1u;
+        const uint64_t i = g0 + lane * step;
+        const uint64_t dm = __ballot(i < p.n && lane < span && p.len[i] >= p.split_len);
+        const uint32_t ns = span < 64u ? static_cast<uint32_t>(span) : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(dm)) >= 3u * ns) skew = p.skew >> 16;
     }
     uint64_t lo64, hi64;
