@@ -82,10 +82,10 @@ def main():
     res["fetch_calibration_bytes_per_counted_byte"] = factors
     bench = res.get("bench", {})
     for name, d in bench.items():
-        # the default C1 kernel only (variant 16: S = 2, D = 1, nt loads); bench.py also launches
-        # its loads-only build (variant 19, ABL 9) for the achievable denominator
-        if (name.startswith("icrc_batch_kernel<0, 2, 1, 8,") or name.startswith("icrc_batch_kernel<0, 2, 1, icrc::anon::Ring<2, true>,")) \
-                and "FETCH_SIZE_KB_mean" in d:
+        # the default C1 kernel only (variant 16: S = 2, D = 1, nt loads, TABLE = false); bench.py
+        # also launches its loads-only build (variant 19, ABL 9) for the achievable denominator and
+        # the small-batch form (TABLE = true: configs[3]'s 4096-packet round trip)
+        if name == "icrc_batch_kernel<0, 2, 1, icrc::anon::Ring<2, true>, false>" and "FETCH_SIZE_KB_mean" in d:
             # the kernel's own shape (256-B dword rows per wave) is membench's rows_chunk / rows_dword
             f = [v for k, v in factors.items() if "rows_chunk" in k or "rows_dword" in k]
             corr = sum(f) / len(f) if f else 2.0
