@@ -10,6 +10,10 @@
 //           4 ds_read_b32 + XOR per word
 //   valu  : table-free, bit-serial GF(2) matrix-vector product: the 32 matrix columns in SGPRs,
 //           per bit one v_bfe_i32 (bit -> all-ones mask) and one 3-input XOR/AND (v_bitop3)
+// lds with C bank copies (price a smaller image first): the byte tables hold C
+// copies (lane l reads copy l % C; C = 32: 128 KiB, conflict-free; 16: 64 KiB; 8: 32 KiB), run with
+// 1024-thread workgroups one per CU, or 512-thread workgroups two per CU (the co-residence an
+// 80 KiB image would allow).
 // Results are folded per lane (acc * (packet | 1)) and written once per wave; XORed over waves on
 // the host, lds and valu must agree bit for bit (the binary checks it).  Not ICRCs (no header mask, no final combine).
 // Build: hipcc --offload-arch=gfx950 -O3 -o stepbench stepbench.hip
@@ -36,17 +40,19 @@ struct Cols {                   // kernel argument: lands in SGPRs
 
 enum { kLoads = 0, kLds = 1, kValu = 2 };
 
-template <int MODE>
+template <int MODE, int C = 32>
 __device__ __forceinline__ uint32_t step(uint32_t acc, const uint32_t *lds, uint32_t lane, const Cols &m) {
     if constexpr (MODE == kLoads) {
         return acc;
     } else if constexpr (MODE == kLds) {
-        const uint32_t l = (lane & 31u) * 4u;
-        const uint32_t a0 = ((acc & 0xFFu) << 7) | l, a1 = (((acc >> 8) & 0xFFu) << 7) | l;
-        const uint32_t a2 = (((acc >> 16) & 0xFFu) << 7) | l, a3 = ((acc >> 24) << 7) | l;
+        constexpr int SH = C == 32 ? 7 : C == 16 ? 6 : 5;  // log2(C * 4): bytes per table entry row
+        constexpr uint32_t TB = 256u * C * 4u;              // bytes per byte table
+        const uint32_t l = (lane & (C - 1u)) * 4u;
+        const uint32_t a0 = ((acc & 0xFFu) << SH) | l, a1 = (((acc >> 8) & 0xFFu) << SH) | l;
+        const uint32_t a2 = (((acc >> 16) & 0xFFu) << SH) | l, a3 = ((acc >> 24) << SH) | l;
         const char *t = reinterpret_cast<const char *>(lds);
-        return *reinterpret_cast<const uint32_t *>(t + a0) ^ *reinterpret_cast<const uint32_t *>(t + 32768 + a1) ^
-               *reinterpret_cast<const uint32_t *>(t + 65536 + a2) ^ *reinterpret_cast<const uint32_t *>(t + 98304 + a3);
+        return *reinterpret_cast<const uint32_t *>(t + a0) ^ *reinterpret_cast<const uint32_t *>(t + TB + a1) ^
+               *reinterpret_cast<const uint32_t *>(t + 2 * TB + a2) ^ *reinterpret_cast<const uint32_t *>(t + 3 * TB + a3);
     } else {
         uint32_t r = 0;
 #pragma unroll
@@ -58,13 +64,13 @@ __device__ __forceinline__ uint32_t step(uint32_t acc, const uint32_t *lds, uint
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(1024) void rows_kernel(const uint32_t *base, uint32_t n, const uint32_t *tables, Cols m,
-                                                    uint32_t *out) {
+template <int MODE, int C = 32, int BS = 1024>
+__global__ __launch_bounds__(BS) void rows_kernel(const uint32_t *base, uint32_t n, const uint32_t *tables, Cols m,
+                                                  uint32_t *out) {
     extern __shared__ uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     if constexpr (MODE == kLds) {
-        for (uint32_t i = threadIdx.x; i < 32768u; i += blockDim.x) lds[i] = tables[i];
+        for (uint32_t i = threadIdx.x; i < 1024u * C; i += blockDim.x) lds[i] = tables[(i / C) * 32u + (i % C)];
         __syncthreads();
     }
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(1024) void rows_kernel(const uint32_t *base, uint32
         for (int r = 0; r < kRows; ++r) nxt[r] = __builtin_nontemporal_load(pn + r * kW);
         uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) acc = step<MODE>(acc, lds, lane, m) ^ cur[r];
+        for (int r = 0; r < kRows; ++r) acc = step<MODE, C>(acc, lds, lane, m) ^ cur[r];
         total ^= acc * (q | 1u);
 #pragma unroll
         for (int r = 0; r < kRows; ++r) cur[r] = nxt[r];
@@ -133,15 +139,19 @@ int main() {
     }
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(rows_kernel<kLds>),
                            hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(rows_kernel<kLds, 16>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(rows_kernel<kLds, 16, 512>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     std::vector<uint32_t> ref;
-    auto run = [&](const char *name, auto kern, int grid, size_t shm, bool check) {
+    auto run = [&](const char *name, auto kern, int grid, size_t shm, bool check, int bs = 1024) {
         CK(hipMemset(out, 0, nout * 4));
-        kern<<<grid, 1024, shm>>>(d, n, t, m, out);
+        kern<<<grid, bs, shm>>>(d, n, t, m, out);
         CK(hipDeviceSynchronize());
-        std::vector<uint32_t> all(static_cast<size_t>(grid) * 16 * 64), h(64, 0u);
+        std::vector<uint32_t> all(static_cast<size_t>(grid) * (bs / 64) * 64), h(64, 0u);
         CK(hipMemcpy(all.data(), out, all.size() * 4, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < all.size(); ++i) h[i & 63] ^= all[i];  // per lane, over all packets: grid-independent
         int agree = -1;
@@ -151,7 +161,7 @@ int main() {
         }
         const int reps = 10;
         CK(hipEventRecord(a));
-        for (int r = 0; r < reps; ++r) kern<<<grid, 1024, shm>>>(d, n, t, m, out);
+        for (int r = 0; r < reps; ++r) kern<<<grid, bs, shm>>>(d, n, t, m, out);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -161,11 +171,19 @@ int main() {
                ms, bytes / (ms * 1e-3) / 1e9, agree);
         fflush(stdout);
     };
+    const bool banks_only = getenv("STEPBENCH_BANKS") != nullptr;  // only the bank-copy rows
     for (int round = 0; round < 2; ++round) {
         run("loads", rows_kernel<kLoads>, cus, 0, false);
         run("lds tables (product step)", rows_kernel<kLds>, cus, 131072, true);
-        run("valu bit-serial (table-free)", rows_kernel<kValu>, cus, 0, true);
-        run("valu bit-serial (table-free), 2 WG/CU", rows_kernel<kValu>, 2 * cus, 0, true);
+        if (!banks_only) {
+            run("valu bit-serial (table-free)", rows_kernel<kValu>, cus, 0, true);
+            run("valu bit-serial (table-free), 2 WG/CU", rows_kernel<kValu>, 2 * cus, 0, true);
+        }
+        run("loads, 512-thread WG x 2 / CU", rows_kernel<kLoads, 32, 512>, 2 * cus, 0, false, 512);
+        run("lds 16 bank copies (64 KiB), 1024-thread WG / CU", rows_kernel<kLds, 16>, cus, 65536, true);
+        run("lds 16 bank copies (64 KiB), 512-thread WG x 2 / CU", rows_kernel<kLds, 16, 512>, 2 * cus, 65536, true, 512);
+        run("lds 8 bank copies (32 KiB), 1024-thread WG / CU", rows_kernel<kLds, 8>, cus, 32768, true);
+        run("lds 8 bank copies (32 KiB), 512-thread WG x 2 / CU", rows_kernel<kLds, 8, 512>, 2 * cus, 32768, true, 512);
     }
     CK(hipFree(d));
     CK(hipFree(t));
