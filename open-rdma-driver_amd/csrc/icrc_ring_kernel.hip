@@ -36,9 +36,6 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t *p) {
 __device__ __forceinline__ void sys_store(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint32_t dev_load(const uint32_t *p) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 template <class T>
 __device__ __forceinline__ void dev_store(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
