@@ -78,9 +78,10 @@ def parse(argv=None):
                     help="per rank: packets at each end of the shard checked against the CPU restatement")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the configs[2] / configs[3] legs of the default line (N = 1)")
-    ap.add_argument("--only", choices=("c2", "rx", "msg"), default=None,
+    ap.add_argument("--only", choices=("c2", "rx", "msg", "host"), default=None,
                     help="run one secondary leg alone and print it: c2 = the configs[2] kernel (rocprofv3 --pmc "
-                         "passes), rx = the short-packet / configs[2] receive legs, msg = the per-message host legs")
+                         "passes), rx = the short-packet / configs[2] receive legs, msg = the per-message host legs, "
+                         "host = the host-resident (PCIe) rate")
     ap.add_argument("--extra", action="store_true",
                     help="also time verify, trailer stores, mixed-MTU, 16 MiB round trip, packetizer, receive "
                          "parse and the host-resident path")
@@ -276,6 +277,10 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         msg = host_message_c0(eng, stream, args)
         print(json.dumps(msg), flush=True)
         return 0
+    if args.only == "host":
+        hr = host_resident(eng, stream, args)
+        print(json.dumps(hr), flush=True)
+        return 0 if hr.get("host_resident_results_match_device", False) else 1
 
     # ---- C1 workload: weak = one QP stream per rank; strong = a shard of one stream ----
     if args.scaling == "weak":
