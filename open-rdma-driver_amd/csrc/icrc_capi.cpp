@@ -1464,3 +1464,33 @@ int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords) {
 }
 
 }  // extern "C"
+
+// Test hook (not in include/icrc.h): `threads` callers each run `jobs` copy-pool jobs of 1..300
+// tasks at once; every task of every job must run exactly once and each job must return only
+// after all of its tasks (the per-job counters of CopyPool).  0 = as specified.
+extern "C" int icrc_copy_pool_selftest(int threads, int jobs) {
+    if (threads < 1 || jobs < 1) return -1;
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int k = 0; k < threads; ++k)
+        th.emplace_back([&, k] {
+            uint32_t x = 0x9E3779B9u * static_cast<uint32_t>(k + 1);
+            for (int j = 0; j < jobs; ++j) {
+                x ^= x << 13;
+                x ^= x >> 17;
+                x ^= x << 5;
+                const uint32_t n = 1u + x % 300u;
+                std::vector<std::atomic<uint32_t>> hits(n);
+                for (auto &h : hits) h.store(0);
+                CopyPool::get().run(n, [&](uint32_t t) {
+                    for (volatile int spin = 0; spin < static_cast<int>(t % 7u) * 50; spin = spin + 1) {
+                    }
+                    hits[t].fetch_add(1);
+                });
+                for (auto &h : hits)
+                    if (h.load() != 1u) bad.fetch_add(1);
+            }
+        });
+    for (auto &t : th) t.join();
+    return bad.load() == 0 ? 0 : 1;
+}

@@ -180,6 +180,7 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "icrc_engine_set_host_path": (i32, [vp, i32]),
         "icrc_engine_host_stats": (i32, [vp, ctypes.POINTER(u64)]),
         "icrc_ring_selftest": (i32, [i32, i32, i32]),  # test hook, not in include/icrc.h
+        "icrc_copy_pool_selftest": (i32, [i32, i32]),  # test hook, not in include/icrc.h
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -387,6 +388,12 @@ def ring_selftest(scenario: int, threads: int = 3, jobs_per_thread: int = 200) -
     """The submission ring's host protocol against a simulated service kernel on a CPU thread
     (icrc_ring_selftest, a test hook of the library): 0 = the scenario behaved as specified."""
     return lib.icrc_ring_selftest(scenario, threads, jobs_per_thread)
+
+
+def copy_pool_selftest(threads: int = 4, jobs: int = 200) -> int:
+    """The host copy pool that gathers pageable host batches (icrc_copy_pool_selftest, a test
+    hook): callers running jobs at once, every task exactly once per job.  0 = as specified."""
+    return lib.icrc_copy_pool_selftest(threads, jobs)
 
 
 class Engine:

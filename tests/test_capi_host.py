@@ -482,3 +482,13 @@ def test_compact_table_replicates_to_the_lds_image(W):
     lds[fin:] = comp[1024:]
     np.testing.assert_array_equal(lds, full)
     assert np.array_equal(icrc_amd.table_image(width=W), full)
+
+
+def test_host_copy_pool():
+    """The pool that gathers pageable host batches into pinned staging (icrc_capi.cpp CopyPool):
+    several callers at once, jobs of 1..300 tasks, every task exactly once and every job complete
+    when its call returns (per-job counters: a worker leaving one job never runs another's task)."""
+    import icrc_amd
+
+    assert icrc_amd.copy_pool_selftest(4, 300) == 0
+    assert icrc_amd.copy_pool_selftest(1, 50) == 0
