@@ -34,7 +34,7 @@
  *     slot of the calling thread).  By default (ICRC_HOST_RING) a message is a job in the engine's
  *     submission ring: a resident service kernel polls the ring's slots in pinned host memory (the
  *     emulator's doorbell / descriptor-queue model, queues/send/queue.rs:66-100), so a call costs
- *     no kernel launch; the kernel (two workgroups per slot: 8 CUs) ends between jobs after 1 ms
+ *     no kernel launch; the kernel (eight 256-thread workgroups per slot: 32 CUs) ends between jobs after 1 ms
  *     of life or 2 ms without calls and the next call starts it again, and a job not done within
  *     2 s fails with ICRC_ETIMEDOUT.  Up to four messages run at once (the emulator's three
  *     threads each get one); more callers wait for a slot.  ICRC_HOST_LAUNCH

@@ -857,6 +857,11 @@ icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
     // measurement knobs (scripts/msg_probe): the ring's shape
     if (const char *v = std::getenv("ICRC_RING_SLOTS")) nslots = static_cast<uint32_t>(std::max(1, std::min(16, std::atoi(v))));
     if (const char *v = std::getenv("ICRC_RING_WGS")) wgs = static_cast<uint32_t>(std::max(1, std::min(32, std::atoi(v))));
+    uint32_t threads = icrc::kRingThreads;
+    if (const char *v = std::getenv("ICRC_RING_THREADS")) {
+        const int t = std::atoi(v);
+        threads = (t == 256 || t == 512 || t == 1024) ? static_cast<uint32_t>(t) : threads;
+    }
     wgs = std::min<uint32_t>(wgs, std::max<uint32_t>(1u, static_cast<uint32_t>(e->num_cu) / nslots));
     // one coherent, device-mapped block: slot lines | done words | exited words | per slot (off, len, res)
     const size_t words = static_cast<size_t>(nslots) * wgs;  // one done / exited word per workgroup
@@ -917,6 +922,7 @@ icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
     r->dev.rp.decision = reinterpret_cast<icrc::RingSlot *>(r->d_mem + d_dec);
     r->dev.rp.table = e->d_table;
     r->dev.rp.wg_per_slot = wgs;
+    r->dev.rp.threads = threads;
     r->dev.rp.idle_ticks = kRingIdleTicks;
     r->dev.rp.life_ticks = kRingLifeTicks;
     if (const char *v = std::getenv("ICRC_RING_LIFE_US"))  // measurement knob: 100 us .. 20 ms

@@ -165,8 +165,11 @@ constexpr uint32_t kRingStop = 0x80000000u;  // RingSlot::cmd: every wave exits
 constexpr uint32_t kRingMaxPackets = 1024u;  // packets per job (one message)
 constexpr uint32_t kRingMaxSlots = 16u;
 constexpr uint32_t kRingSlots = 4u;          // default: one per emulator thread (3) + one
-constexpr uint32_t kRingWgPerSlot = 2u;      // default workgroups per slot (CUs reading one message):
-                                             // 2 beat 4 and 8 from 3-4 threads (profiles/r05/ring/)
+// Default shape: 8 workgroups of 256 threads per slot, i.e. a message's loads spread over 8 CUs
+// (one CU pulls host memory at ~25 GB/s, four at ~56: scripts/hostreadbench.hip), 32 CUs in all.
+// 3 threads 64-65 K messages/s against 56-57 K for 2 x 1024 (profiles/r05/ring/r05i).
+constexpr uint32_t kRingThreads = 256u;      // default workgroup size of the service kernel
+constexpr uint32_t kRingWgPerSlot = 8u;      // default workgroups per slot (CUs reading one message)
 struct alignas(64) RingSlot {  // host-written, one 64-byte line per slot
     uint32_t cmd;       // job number (bits 0-30, never 0 for a job) | kRingStop; written last
     uint32_t activity;  // the host's submission counter, copied into every slot on every call
@@ -207,6 +210,8 @@ struct RingParams {
     RingSlot *decision;     // device memory [slot][wg]: wave 0's decision (the job, or kRingStop)
     const uint32_t *table;  // W = 64 table buffer (image + compact form)
     uint32_t wg_per_slot;
+    uint32_t threads;       // workgroup size, 256 / 512 / 1024: one workgroup per CU either way (the
+                            // 160 KiB table image), so fewer threads spread a job over more CUs
     uint32_t epoch;         // launch number
     uint32_t idle_ticks;    // s_memrealtime ticks (100 MHz) without host activity before exiting
     uint32_t life_ticks;    // ... and since the launch: a launch ends at a job boundary after this long,

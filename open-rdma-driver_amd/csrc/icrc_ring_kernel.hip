@@ -52,9 +52,30 @@ __device__ __forceinline__ uint64_t line_u64(uint32_t v, int dword) {
     return static_cast<uint64_t>(readlane_u32(v, dword)) | (static_cast<uint64_t>(readlane_u32(v, dword + 1)) << 32);
 }
 
-__global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams rp) {
+// The W = 64 table image into LDS from its compact form (table_fill's work, icrc_device.h, for a
+// workgroup of NT threads: each thread takes the shares of threads t, t + NT, ...).
+template <int NT>
+__device__ __forceinline__ void ring_table_fill(uint4 *lds4, const uint32_t *table) {
+    const uint32_t *cf = table + kLdsWords;
+    for (uint32_t v = threadIdx.x; v < 1024u; v += NT) {
+        const uint32_t bulk = cf[v];
+        const uint32_t b = v >> 8, x = v & 255u;
+        const uint32_t row = ((b >> 1) * 65536u + x * 256u + (b & 1u) * 128u) / 16u;
+        const uint4 q = make_uint4(bulk, bulk, bulk, bulk);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) lds4[row + ((k + x) & 7u)] = q;
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k)
+            lds4[kFinalBase / 16u + v + k * 1024u] = reinterpret_cast<const uint4 *>(cf + 1024u)[v + k * 1024u];
+    }
+    __syncthreads();
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void icrc_ring_kernel(RingParams rp) {
+    constexpr uint32_t kWaves = NT / 64;
     __shared__ uint4 lds4[kLdsBytes / 16];
-    table_fill(lds4, rp.table);  // ends in a barrier
+    ring_table_fill<NT>(lds4, rp.table);  // ends in a barrier
     const char *lds = reinterpret_cast<const char *>(lds4);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -140,9 +161,9 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams 
         p.table = rp.table;
         p.skew = 0u;
         if (n <= kRingMaxPackets && !(rp.ab & 8u)) {  // the host never posts more; a corrupt line does nothing
-            const uint32_t nwaves = rp.wg_per_slot * kWavesPerGroup;
+            const uint32_t nwaves = rp.wg_per_slot * kWaves;
             const uint32_t chunk = (n + nwaves - 1u) / nwaves;
-            const uint32_t w = sub * kWavesPerGroup + wave;
+            const uint32_t w = sub * kWaves + wave;
             const uint32_t lo = w * chunk < n ? w * chunk : n;
             const uint32_t nq = (n - lo) < chunk ? (n - lo) : chunk;
             run_pipelined<kCompute, 2, 1, RingHostResults>(p, lds, c, lane, lo, nq);
@@ -174,8 +195,14 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_ring_kernel(RingParams 
 
 int launch_ring(const RingParams &rp, uint32_t nslots, void *stream) {
     if (nslots == 0 || rp.wg_per_slot == 0) return ICRC_EINVAL;
-    hipLaunchKernelGGL(icrc_ring_kernel, dim3(nslots * rp.wg_per_slot), dim3(kThreadsPerGroup), 0,
-                       static_cast<hipStream_t>(stream), rp);
+    const dim3 g(nslots * rp.wg_per_slot);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (rp.threads) {
+    case 256: hipLaunchKernelGGL(icrc_ring_kernel<256>, g, dim3(256), 0, s, rp); break;
+    case 512: hipLaunchKernelGGL(icrc_ring_kernel<512>, g, dim3(512), 0, s, rp); break;
+    case 1024: hipLaunchKernelGGL(icrc_ring_kernel<1024>, g, dim3(1024), 0, s, rp); break;
+    default: return ICRC_EINVAL;
+    }
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
