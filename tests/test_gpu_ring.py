@@ -212,3 +212,33 @@ def test_ring_does_not_hold_back_other_streams():
         stop.set()
         th.join(timeout=60)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("threads,wgs", [(256, 8), (512, 4), (1024, 2), (256, 1)])
+def test_ring_workgroup_shapes(threads, wgs, monkeypatch):
+    """Every instantiation of the service kernel (ICRC_RING_THREADS 256 / 512 / 1024, read when an
+    engine's ring is created): C0 messages and ragged batches up to the 1024-packet cap, pinned and
+    pageable, bit-exact against the oracle, verify catching a flipped bit, all through the ring."""
+    import icrc_amd
+
+    monkeypatch.setenv("ICRC_RING_THREADS", str(threads))
+    monkeypatch.setenv("ICRC_RING_WGS", str(wgs))
+    eng = icrc_amd.Engine(0)
+    try:
+        rng = np.random.default_rng(threads + wgs)
+        keep = []
+        cases = [c0_message(5), ragged_message(rng, 1024), ragged_message(rng, 3), ragged_message(rng, 257)]
+        for k, (ref, off, lens) in enumerate(cases):
+            want = oracle.compute_icrc_batch(ref, np.asarray(off, np.uint64), np.asarray(lens, np.uint32))
+            host = pinned_copy(ref, keep) if k % 2 else ref.copy()
+            np.testing.assert_array_equal(eng.compute_batch_host(host, off, lens, write_trailer=True), want)
+            bad = int(rng.integers(0, len(lens)))
+            host[int(off[bad]) + 50] ^= 0x01
+            ok = eng.verify_batch_host(host, off, lens, zero_trailer=False)
+            expect = np.ones(len(lens), np.uint8)
+            expect[bad] = 0
+            np.testing.assert_array_equal(ok, expect)
+        st = eng.host_stats()
+        assert st["jobs"] == 2 * len(cases) and st["timeouts"] == 0, st
+    finally:
+        eng.close()
