@@ -207,6 +207,20 @@ def _check(rc: int, what: str) -> None:
         raise IcrcError(rc, what)
 
 
+_CHAR = ctypes.c_char
+
+
+def _ptr(a: np.ndarray) -> int:
+    """The address of an ndarray's data.  ctypes.c_char.from_buffer is ~4x cheaper than
+    a.ctypes.data (which builds a helper object on every access) — the host-message calls take four
+    pointers each, and every microsecond spent here is spent holding the GIL, which the other
+    Python callers wait for.  Read-only or empty arrays take the ctypes.data path."""
+    try:
+        return ctypes.addressof(_CHAR.from_buffer(a))
+    except (TypeError, ValueError, BufferError):
+        return a.ctypes.data
+
+
 def _u8(a, writable: bool = False) -> np.ndarray:
     """A uint8 view of `a` WITHOUT copying (ndarray, bytearray, memoryview, bytes ...), so that
     in-place effects (is_icrc_valid's trailer zeroing, trailer writes) reach the caller's buffer.
@@ -256,7 +270,7 @@ def compute_icrc(data) -> int:
     reference would panic (len < 44)."""
     a = _u8(data)
     err = ctypes.c_int(0)
-    v = lib.icrc_compute(a.ctypes.data, a.size, ctypes.byref(err))
+    v = lib.icrc_compute(_ptr(a), a.size, ctypes.byref(err))
     _check(err.value, "compute_icrc")
     return v
 
@@ -267,7 +281,7 @@ def is_icrc_valid(buf, zero_trailer: bool = True) -> bool:
     (ndarray, bytearray, memoryview); a read-only one raises TypeError when zero_trailer."""
     a = _u8(buf, writable=zero_trailer)
     ok = ctypes.c_int(0)
-    _check(lib.icrc_verify(a.ctypes.data, a.size, 1 if zero_trailer else 0, ctypes.byref(ok)),
+    _check(lib.icrc_verify(_ptr(a), a.size, 1 if zero_trailer else 0, ctypes.byref(ok)),
            "is_icrc_valid")
     return bool(ok.value)
 
@@ -346,8 +360,8 @@ def compute_icrc_batch(base: np.ndarray, off, lens, write_trailer: bool = False)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     out = np.zeros(off.size, dtype=np.uint32)
-    _check(lib.icrc_compute_batch(_u8(base, writable=write_trailer).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
-                                  out.ctypes.data, 1 if write_trailer else 0), "icrc_compute_batch")
+    _check(lib.icrc_compute_batch(_ptr(_u8(base, writable=write_trailer)), _ptr(off), _ptr(lens), off.size,
+                                  _ptr(out), 1 if write_trailer else 0), "icrc_compute_batch")
     return out
 
 
@@ -355,8 +369,8 @@ def verify_icrc_batch(base: np.ndarray, off, lens, zero_trailer: bool = False) -
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     ok = np.zeros(off.size, dtype=np.uint8)
-    _check(lib.icrc_verify_batch(_u8(base, writable=zero_trailer).ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
-                                 ok.ctypes.data, 1 if zero_trailer else 0), "icrc_verify_batch")
+    _check(lib.icrc_verify_batch(_ptr(_u8(base, writable=zero_trailer)), _ptr(off), _ptr(lens), off.size,
+                                 _ptr(ok), 1 if zero_trailer else 0), "icrc_verify_batch")
     return ok
 
 
