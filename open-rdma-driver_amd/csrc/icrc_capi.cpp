@@ -170,6 +170,7 @@ struct DispatchKnobs {
     int hybrid_seq = 0;          // ICRC_AB_HYBRID_SEQ: 1 / 2 = the halves as two kernels in a row (oct / long first)
     int long_grid_mult = 1;      // ICRC_AB_LONG_GRID: long-packet workgroups per oct workgroup
     int long_cus = 0;            // ICRC_AB_LONG_CUS: CUs running long-packet workgroups from the start
+    int long_self = 1;           // ICRC_AB_LONG_SELF=0: the two workgroup sets (oct, then long-packet ones)
 };
 DispatchKnobs dispatch_knobs() {
     DispatchKnobs k;
@@ -186,6 +187,7 @@ DispatchKnobs dispatch_knobs() {
     k.hybrid_seq = env("ICRC_AB_HYBRID_SEQ", 0);
     k.long_grid_mult = std::max(1, env("ICRC_AB_LONG_GRID", 1));
     k.long_cus = env("ICRC_AB_LONG_CUS", 0);
+    k.long_self = env("ICRC_AB_LONG_SELF", 1);
 #endif
     return k;
 }
@@ -242,6 +244,7 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
             return rc;
         }
         if (k.long_cus > 0 && k.long_cus < grid) return icrc::launch_hybrid(mode, p, grid - k.long_cus, k.long_cus, stream);
+        if (k.long_self) return icrc::launch_hybrid(mode, p, grid, 0, stream);
         return icrc::launch_hybrid(mode, p, grid, grid * k.long_grid_mult, stream);
     }
     std::lock_guard<std::mutex> g(e->fork_mu);

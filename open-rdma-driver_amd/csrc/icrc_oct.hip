@@ -704,6 +704,18 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_kernel(BatchPara
     if (blockIdx.x < g_oct) oct_body<MODE, true, TRAILER, OctProduct>(p, lds4, blockIdx.x, g_oct);
     else long_body<MODE, COMPACT, TRAILER, LA>(p, lds4, blockIdx.x - g_oct, gridDim.x - g_oct);
 }
+// The default ragged dispatch (round 5): ONE set of #CUs workgroups; each runs its oct range, then
+// reloads LDS with the W = 64 image and walks the long packets of the same range itself.  Against
+// the two sets above (the long-packet workgroups taking CUs as the oct ones retire): configs[2]
+// -1.5 %, C1's packets as a ragged batch -0.6 %, identical results (scripts/probe_long_self.py,
+// profiles/r05/c2/long_self_ab.jsonl): no second dispatch of 160 KiB workgroups, no tail of them.
+template <int MODE, bool TRAILER, bool COMPACT>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_self_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    oct_body<MODE, true, TRAILER, OctProduct>(p, lds4, blockIdx.x, gridDim.x);
+    __syncthreads();  // every wave is done with the oct image before the long body rewrites LDS
+    long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x, gridDim.x);
+}
 #ifdef ICRC_AB_BUILD
 // A/B (ICRC_AB_HYBRID_STAMP=1, compute): the hybrid kernel with each workgroup's start and end
 // (s_memrealtime, 100 MHz) and kind stored in g_hybrid_stamps, entry b = {start lo, start hi, end
@@ -792,6 +804,16 @@ int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, v
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 g(static_cast<uint32_t>(grid_oct + grid_long));
     const uint32_t go = static_cast<uint32_t>(grid_oct);
+    if (grid_long == 0) {  // the default: each workgroup both halves of its range (icrc_hybrid_self_kernel)
+        if (mode == kCompute) {
+            if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_self_kernel<kCompute, true, false>), dim3(go), dim3(kThreadsPerGroup), 0, s, p);
+            else hipLaunchKernelGGL((icrc_hybrid_self_kernel<kCompute, false, false>), dim3(go), dim3(kThreadsPerGroup), 0, s, p);
+        } else {
+            if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_self_kernel<kVerify, true, false>), dim3(go), dim3(kThreadsPerGroup), 0, s, p);
+            else hipLaunchKernelGGL((icrc_hybrid_self_kernel<kVerify, false, false>), dim3(go), dim3(kThreadsPerGroup), 0, s, p);
+        }
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
 #define ICRC_H(M, T, C) hipLaunchKernelGGL((icrc_hybrid_kernel<M, T, C>), g, dim3(kThreadsPerGroup), 0, s, p, go)
 #define ICRC_HM(M)                                    \
     do {                                              \

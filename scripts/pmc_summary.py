@@ -99,9 +99,11 @@ def main():
                 "write_bytes": round(write), "traffic_bytes": round(fetch + write),
                 "algorithmic_bytes": alg, "ratio_to_algorithmic": round((fetch + write) / alg, 4)}
     # configs[2]: the default one-launch hybrid kernel (compute, no trailer, dense / compacting long
-    # walk by density) over the 4 Mi mixed-MTU batch of bench.py's c2 leg
+    # walk by density; since round 5 each workgroup walks its own range's long packets:
+    # icrc_hybrid_self_kernel) over the 4 Mi mixed-MTU batch of bench.py's c2 leg
     for name, d in bench.items():
-        if name.startswith("icrc_hybrid_kernel<0, false, false") and "FETCH_SIZE_KB_mean" in d:
+        if (name.startswith("icrc_hybrid_self_kernel<0, false, false") or name.startswith("icrc_hybrid_kernel<0, false, false")) \
+                and "FETCH_SIZE_KB_mean" in d:
             sys.path.insert(0, os.path.join(ROOT, "open-rdma-driver_amd"))
             from icrc_amd import workloads  # noqa: E402
 
