@@ -171,6 +171,7 @@ struct DispatchKnobs {
     int long_grid_mult = 1;      // ICRC_AB_LONG_GRID: long-packet workgroups per oct workgroup
     int long_cus = 0;            // ICRC_AB_LONG_CUS: CUs running long-packet workgroups from the start
     int long_self = 1;           // ICRC_AB_LONG_SELF=0: the two workgroup sets (oct, then long-packet ones)
+    int self_grid_mult = 1;      // ICRC_AB_SELF_GRID: workgroups per CU of the in-place hybrid (smaller ranges)
 };
 DispatchKnobs dispatch_knobs() {
     DispatchKnobs k;
@@ -188,6 +189,7 @@ DispatchKnobs dispatch_knobs() {
     k.long_grid_mult = std::max(1, env("ICRC_AB_LONG_GRID", 1));
     k.long_cus = env("ICRC_AB_LONG_CUS", 0);
     k.long_self = env("ICRC_AB_LONG_SELF", 1);
+    k.self_grid_mult = std::max(1, std::min(8, env("ICRC_AB_SELF_GRID", 1)));
 #endif
     return k;
 }
@@ -244,7 +246,7 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
             return rc;
         }
         if (k.long_cus > 0 && k.long_cus < grid) return icrc::launch_hybrid(mode, p, grid - k.long_cus, k.long_cus, stream);
-        if (k.long_self) return icrc::launch_hybrid(mode, p, grid, 0, stream);
+        if (k.long_self) return icrc::launch_hybrid(mode, p, grid * k.self_grid_mult, 0, stream);
         return icrc::launch_hybrid(mode, p, grid, grid * k.long_grid_mult, stream);
     }
     std::lock_guard<std::mutex> g(e->fork_mu);

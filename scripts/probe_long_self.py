@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""A/B: the hybrid launch's long packets walked by separately dispatched long-packet workgroups
-(the default) or by each oct workgroup itself after its oct range (ICRC_AB_LONG_SELF=1, A/B
-library: the W = 64 image reloaded into LDS, no second wave of workgroups, no tail).  One process,
+"""A/B: the hybrid launch's long packets walked by a second set of long-packet workgroups
+(ICRC_AB_LONG_SELF=0, the round-4 form) or by each workgroup itself after its oct range (the
+default since round 5: the W = 64 image reloaded into LDS, no second set, no tail); FORMS picks
+the forms ("0", "1", "s2" = in place with 2 x #CUs workgroups, ...).  One process,
 alternating rounds; configs[2], C1's packets as a ragged batch, the 316-B class alone; the results
 of both forms must be identical.  One JSON line per (batch, form): median ms of ROUNDS x 10 launches."""
 import json
@@ -31,12 +32,14 @@ def main():
         b = workloads.synthesize(eng, w, stream=s)
         off = torch.from_numpy(np.ascontiguousarray(w.off)).cuda()
         ln = torch.from_numpy(np.ascontiguousarray(w.lens)).cuda()
-        out = {f: torch.zeros(w.n, dtype=torch.int32, device="cuda") for f in ("0", "1")}
-        ms = {"0": [], "1": []}
+        forms = os.environ.get("FORMS", "0,1").split(",")  # LONG_SELF value, or "s<k>": in place, k x #CUs workgroups
+        out = {f: torch.zeros(w.n, dtype=torch.int32, device="cuda") for f in forms}
+        ms = {f: [] for f in forms}
         tot = int(w.lens.astype(np.uint64).sum())
         for r in range(rounds):
-            for f in ("0", "1"):
-                os.environ["ICRC_AB_LONG_SELF"] = f
+            for f in forms:
+                os.environ["ICRC_AB_LONG_SELF"] = "1" if f.startswith("s") else f
+                os.environ["ICRC_AB_SELF_GRID"] = f[1:] if f.startswith("s") else "1"
                 fn = lambda: eng.compute_batch(b.data_ptr(), off.data_ptr(), ln.data_ptr(), w.n,  # noqa: E731
                                                out[f].data_ptr(), False, 0, s)
                 for _ in range(3):
@@ -49,15 +52,16 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 ms[f].append(a.elapsed_time(e) / 10)
-        same = bool(torch.equal(out["0"], out["1"]))
-        for f in ("0", "1"):
+        same = all(bool(torch.equal(out[forms[0]], out[f])) for f in forms)
+        for f in forms:
             m = float(np.median(ms[f]))
-            print(json.dumps({"batch": name, "long_self": int(f), "ms_median": round(m, 4),
+            print(json.dumps({"batch": name, "form": f, "ms_median": round(m, 4),
                               "ms_all": [round(x, 4) for x in ms[f]], "frac_of_8TB/s": round(tot / (m * 1e-3) / 8e12, 4),
                               "results_identical": same}), flush=True)
         del b, off, ln, out
         torch.cuda.empty_cache()
     os.environ.pop("ICRC_AB_LONG_SELF", None)
+    os.environ.pop("ICRC_AB_SELF_GRID", None)
 
 
 if __name__ == "__main__":
