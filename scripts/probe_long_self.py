@@ -2,7 +2,8 @@
 """A/B: the hybrid launch's long packets walked by a second set of long-packet workgroups
 (ICRC_AB_LONG_SELF=0, the round-4 form) or by each workgroup itself after its oct range (the
 default since round 5: the W = 64 image reloaded into LDS, no second set, no tail); FORMS picks
-the forms ("0", "1", "s2" = in place with 2 x #CUs workgroups, ...).  One process,
+the forms ("0", "1", "s2" = in place with 2 x #CUs workgroups, "k45" = in place with oct wave
+skew 45, ...).  One process,
 alternating rounds; configs[2], C1's packets as a ragged batch, the 316-B class alone; the results
 of both forms must be identical.  One JSON line per (batch, form): median ms of ROUNDS x 10 launches."""
 import json
@@ -38,8 +39,12 @@ def main():
         tot = int(w.lens.astype(np.uint64).sum())
         for r in range(rounds):
             for f in forms:
-                os.environ["ICRC_AB_LONG_SELF"] = "1" if f.startswith("s") else f
+                os.environ["ICRC_AB_LONG_SELF"] = "1" if f[0] in "sk" else f
                 os.environ["ICRC_AB_SELF_GRID"] = f[1:] if f.startswith("s") else "1"
+                if f.startswith("k"):  # "k<e>": in place, oct wave skew e (ICRC_AB_SKEW_OCT)
+                    os.environ["ICRC_AB_SKEW_OCT"] = f[1:]
+                else:
+                    os.environ.pop("ICRC_AB_SKEW_OCT", None)
                 fn = lambda: eng.compute_batch(b.data_ptr(), off.data_ptr(), ln.data_ptr(), w.n,  # noqa: E731
                                                out[f].data_ptr(), False, 0, s)
                 for _ in range(3):
@@ -62,6 +67,7 @@ def main():
         torch.cuda.empty_cache()
     os.environ.pop("ICRC_AB_LONG_SELF", None)
     os.environ.pop("ICRC_AB_SELF_GRID", None)
+    os.environ.pop("ICRC_AB_SKEW_OCT", None)
 
 
 if __name__ == "__main__":
