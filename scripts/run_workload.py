@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Run one workload a few times with the default dispatch (for rocprofv3 --pmc / --stats).
 
-usage: run_workload.py {c1,c1w,c1v,c1vz,c2,c2nr,c2s,c2k,c2m,c3,s316,packetize} [launches] [variant]
+usage: run_workload.py {c1,c1w,c1v,c1vz,c2,c2nr,c2s,c2k,c2m,c3,s316,rx316,rx316r,packetize} [launches] [variant]
   c2nr / c2s / c2k / c2m: C2 without ragged LAST packets / only the 256-B class / only the
   1 KiB class / 256-B and 1 KiB classes (4 Mi packets each, packed, offset / length arrays);
   c1w: C1 compute with write_trailer; c1v / c1vz: C1 verify without / with zero_trailer; s316: 4 Mi strided
-  316-byte packets; packetize: the fused send packetizer over 192 x 16 MiB WRITE messages
+  316-byte packets; rx316 / rx316r: icrc_rx_parse_device over those packets (trailers written),
+  strided / as a ragged batch; packetize: the fused send packetizer over 192 x 16 MiB WRITE messages
   (786 K x 4156-B packets, as bench.py --extra)"""
 import os
 import sys
@@ -27,7 +28,23 @@ def main():
     if len(sys.argv) > 3:
         eng.set_variant(int(sys.argv[3]))
     s = torch.cuda.current_stream().cuda_stream
-    if which in ("c1", "c1w", "c1v", "c1vz", "s316"):
+    if which in ("rx316", "rx316r"):
+        w = workloads.write_middle_stream(1 << 22, pmtu=256)
+        L = int(w.lens[0])
+        b = workloads.synthesize(eng, w, stream=s)
+        o = torch.from_numpy(np.ascontiguousarray(w.off)).cuda()
+        ln = torch.from_numpy(np.ascontiguousarray(w.lens)).cuda()
+        tmp = torch.zeros(w.n, dtype=torch.int32, device="cuda")
+        eng.compute_batch(b.data_ptr(), o.data_ptr(), ln.data_ptr(), w.n, tmp.data_ptr(), True, 0, s)
+        desc = torch.empty(w.n * icrc_amd.RX_DESC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        ok = torch.zeros(w.n, dtype=torch.uint8, device="cuda")
+        if which == "rx316":
+            fn = lambda: eng.rx_parse(b.data_ptr(), 0, 0, w.n, desc.data_ptr(), ok.data_ptr(), stride=L, length=L,  # noqa: E731
+                                      stream=s)
+        else:
+            fn = lambda: eng.rx_parse(b.data_ptr(), o.data_ptr(), ln.data_ptr(), w.n, desc.data_ptr(), ok.data_ptr(),  # noqa: E731
+                                      stream=s)
+    elif which in ("c1", "c1w", "c1v", "c1vz", "s316"):
         w = workloads.write_middle_stream(1 << 22, pmtu=256) if which == "s316" else workloads.write_middle_stream(1 << 20)
         L = int(w.lens[0])
         b = workloads.synthesize(eng, w, stream=s)
