@@ -1348,6 +1348,16 @@ int icrc_synth_device(icrc_engine *e, uint8_t *d_base, const icrc_synth_desc *d_
     return icrc::launch_synth(d_base, d_desc, d_hdr, n, stream);
 }
 
+// ICRC_AB_RX_OCT (A/B library): 0 the two passes, 1 the one pass, 2..5 its cuts (launch_oct_rx).
+static int rx_oct_knob() {
+#ifdef ICRC_AB_BUILD
+    const char *v = std::getenv("ICRC_AB_RX_OCT");
+    return v ? std::atoi(v) : 1;
+#else
+    return 1;
+#endif
+}
+
 int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
                          uint64_t stride, uint32_t len, uint32_t n, icrc_rx_desc *d_desc, uint8_t *d_ok,
                          int zero_trailer, uint32_t *d_nerr, void *stream) {
@@ -1380,6 +1390,14 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     if (e->variant < 0 && n <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup) {
         p.variant = 2;
         return icrc::launch_rx(p, grid_for(e, n), stream);
+    }
+    // Strided batches of short packets: ONE pass (icrc_oct_rx_kernel): the oct verify keeps each
+    // packet's header words as loaded and stores the descriptors itself, so the header lines are not
+    // read twice.  (A/B: ICRC_AB_RX_OCT=0 keeps the two passes.)
+    if (e->variant < 0 && !d_off && !d_len && len >= ICRC_MIN_PACKET && len <= icrc::oct_max_len() && len % 4u == 0 &&
+        stride % 4u == 0 && stride <= (1ull << 24) && reinterpret_cast<uintptr_t>(d_base) % 4u == 0 && rx_oct_knob() != 0) {
+        p.table_oct = e->d_table_oct;
+        return icrc::launch_oct_rx(p, grid_for(e, n), stream, rx_oct_knob());
     }
     // Otherwise two passes (icrc_kernels.hip, icrc_rx_desc_kernel): the verify dispatch writes the
     // ok bytes (into d_ok, or a stream-ordered scratch array when the caller passes none), then the

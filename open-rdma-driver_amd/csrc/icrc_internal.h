@@ -120,6 +120,10 @@ int launch_rx_desc(const BatchParams &p, int num_cu, void *stream);
 // Fixed-frame oct kernel (icrc_oct.hip), variant 40: packets of at most oct_max_len() bytes.
 int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag = 0);
 uint32_t oct_max_len();
+// The fused receive (icrc_oct.hip, icrc_oct_rx_kernel): verify + descriptors in one pass over a
+// strided batch whose packets are all the oct kernel's (44 <= L <= oct_max_len(), 4-aligned).
+// diag (A/B library only, ICRC_AB_RX_OCT=2..5): the kernel's cuts (OctRxAblation, icrc_oct.hip).
+int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag = 0);
 // The hybrid dispatch with the oct kernel as its short-packet half, in one launch (icrc_oct.hip):
 // grid_oct workgroups of the oct kernel, then grid_long of the long-packet kernel.
 int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);

@@ -317,6 +317,12 @@ struct OctProduct {
     static constexpr bool kPrio = true;        // raised wave priority over a frame's setup and loads
     static constexpr bool kReusePrep = false;  // the first block's preparation reused (strided, full blocks)
     static constexpr bool kStamp = false;      // each wave stamps start / end times over its first results
+    static constexpr bool kRxDeposit = true;   // RX: header words into the record
+    static constexpr bool kRxDecode = true;    // RX: the block decode and its stores
+    static constexpr bool kRxStoreOOR = false; // RX: ... its global stores issued out of range (dropped)
+    static constexpr bool kRxWrBarrier = true; // RX: a scheduling barrier after each record write of the decode
+    static constexpr bool kRxX4 = false;       // RX: the descriptors leave as 16-byte stores (else dword stores)
+    static constexpr int kRxStoreAux = kStreamAux;  // RX: the descriptor stores' cache policy (nt: -2.5 %, rx_oct_ab)
 };
 #ifdef ICRC_AB_BUILD
 // 41 loads only; 42 row steps, no loads; 43 control and final products; 44 control only; 45 = 41
@@ -336,9 +342,58 @@ struct OctAblation : OctProduct {
     static constexpr bool kReusePrep = X == 12;
     static constexpr bool kStamp = X == 13;
 };
+// The receive kernel's cuts and alternatives (ICRC_AB_RX_OCT=2..8): 2 no record writes, 3 no block
+// decode / stores, 4 neither (the 16-copy verify alone), 5 the decode with every global store out
+// of range; 6 the descriptor stores without the non-temporal hint, 7 (= the product), 8 16-byte
+// non-temporal descriptor stores.
+template <int X>
+struct OctRxAblation : OctProduct {
+    static constexpr bool kRxDeposit = !(X == 2 || X == 4);
+    static constexpr bool kRxDecode = !(X == 3 || X == 4);
+    static constexpr bool kRxStoreOOR = X == 5;
+    static constexpr bool kRxX4 = X == 8;
+    static constexpr int kRxStoreAux = (X == 6 || X == 5) ? 0 : kStreamAux;
+};
 #endif
 
-template <int MODE, bool RAGGED, bool TRAILER, class D>
+// ---- the fused receive (RX: verify + strip + parse in the oct kernel, icrc_oct_rx_kernel) ------
+// The two-pass receive re-reads every packet's header lines after the verify (~1.4 128-B lines per
+// 316-B packet: 0.18 of its 0.45 ms on 4 Mi x 316 B).  Here the verify waves keep what they load:
+// a set's first frame holds packet words 7..17 (BTH and extension headers) in rows 1..3, and each
+// lane writes its words into the wave's LDS block record; when a block's last set is done the wave
+// decodes its 64 packets lane = packet (rx_decode's fields) IN the record, then stores the 64
+// descriptors (4608 contiguous bytes) as 18 coalesced dword stores.  (Stored lane = packet, 72 B
+// apart, the same descriptors made the pass 2.4x slower than the verify, 16-byte stores 1.6x:
+// profiles/r05/rx_oct_ab.jsonl.)
+//
+// LDS map of the receive kernel: the bulk tables with 16 bank copies in the lower halves of the
+// 512 table rows of 256 B (scripts/stepbench.hip: no slower than 32 copies on the oct shape), the
+// final tables of lanes 0..31 in the upper halves of rows 0..127 (c.fin = 128 + (lane & 31) * 4,
+// final_mul unchanged; lanes l and l + 32 share a bank), and per wave a record of 19 rows of 64
+// packets (row stride 512 B, packets 32..63 256 B on): waves 0..9 in the upper halves of table
+// rows 128..507, waves 10..15 two by two in the old final-table region.  Row k = dword k of the
+// packets' descriptors; before the decode, header word w sits in the row of the dword formed from
+// it (kRxHdrRows), so the decode reads and writes each row in place; row 18 takes a deposit lane's
+// unused writes.  One record per wave: a block's words are written when its sets' first frames are
+// consumed, decoded and stored when its last frame is, and the next block's first frame is
+// consumed after that (consume orders deposit / finish / stores per slot).
+constexpr uint32_t kRxRows = 19u, kRxRecRow = 512u, kRxDummyRow = 18u;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// header word 7 + i -> record row: nibble i (7->15 8->12 9->13 10->14 11->0 12->7 13->8 14->11
+// 15->2 16->9 17->10)
+constexpr uint64_t kRxHdrRows = 0xA92B870EDCFull;
+__device__ __forceinline__ uint32_t rx_wave_base(uint32_t w) {
+    return w < 10u ? (128u + 38u * w) * 256u + 128u
+                   : kFinalBase + ((w - 10u) >> 1) * (kRxRows * kRxRecRow) + ((w - 10u) & 1u) * 128u;
+}
+// Packet i of record row k, rotated by 2 k within its 32-packet half: the decode (lane = packet, one
+// row) reads 32 banks either way, and the transposing read-back -- whose 32 lanes take ~18 rows of
+// two packets -- hits ~2 lanes per bank instead of ~18 (68 LDS cycles over its 18 reads against 640).
+__device__ __forceinline__ uint32_t rx_ent(uint32_t i, uint32_t k) {
+    return k * kRxRecRow + ((i >> 5) << 8) + (((i + 2u * k) & 31u) << 2);
+}
+
+template <int MODE, bool RAGGED, bool TRAILER, class D, bool RX = false>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
                                         uint32_t lo, uint32_t nq) {
     constexpr bool kPrio = kOctPrio && D::kPrio;
@@ -371,7 +426,10 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     bool lreal = false, ldone = false;
     int lkf = 0, lr = 0;
     uint32_t lvrow0 = 0, ltr = kOctOOR;
+    uint32_t lidx = 0;  // RX: the packet's index in its block, | 64 if real
     int inflight = 0;
+    // RX: the wave's record
+    const uint32_t rx_wb = RX ? rx_wave_base(readfirstlane_u32(threadIdx.x >> 6)) : 0u;
 
     OctSlot<MODE, TRAILER> sl[B];
 #pragma unroll
@@ -448,6 +506,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             lkf = col - z;
             lvrow0 = vrel + 4u * static_cast<uint32_t>(lkf - 1);
             ltr = (lreal && col == 0) ? vrel + L - 4u : kOctOOR;
+            if constexpr (RX) lidx = (key & 63u) | (lreal ? 64u : 0u);
         }
         const uint32_t lf = (fd >> 16) & 0xFFu;
         const uint32_t fo = 32u * K * lf;
@@ -486,9 +545,10 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         }
         const bool last = (fd & kOctLast) != 0u;
-        S.kf = lkf;
+        // (RX: the packet's block index in bits 8-13, bit 14 set for a real packet; readers mask & 63)
+        S.kf = RX ? static_cast<int>((static_cast<uint32_t>(lkf) & 63u) | (lidx << 8)) : lkf;
         S.rl = lr - K * static_cast<int>(lf);
-        S.tro = last ? ltr : kOctOOR;
+        if constexpr (!RX) S.tro = last ? ltr : kOctOOR;  // (RX: the block's trailers are zeroed with its descriptors)
         // routing: packet i of the block (pos_i = its sorted position, 0xFF if not this kernel's)
         // takes group (pos_i & 7)'s result at the last frame of set pos_i >> 3
         const uint32_t pi = LB.pos;
@@ -499,6 +559,149 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         S.fl = fd;
         lt += have ? 1 : 0;
         inflight += have ? 1 : 0;
+    };
+
+    // RX: a set's first frame -> its packets' words 7..17 (raw, before the header masks) into the
+    // wave's record.  Lane c of row j holds stream word 8 j + kf = packet word 8 j + kf - 1; it is
+    // written when that is one of 7..17 and not the trailer or past it (row index 8 j + c below
+    // 8 R - 1).  Every lane writes (a lane with nothing to write: its dummy entry), no branch
+    // around an LDS store.
+    auto deposit = [&](const OctSlot<MODE, TRAILER> &S) __attribute__((always_inline)) {
+        if constexpr (RX && D::kRxDeposit) {
+            if (!(S.fl & kOctFirst)) return;
+            char *rec = const_cast<char *>(lds);
+            const uint32_t kx = static_cast<uint32_t>(S.kf);
+            const int kf = static_cast<int>((kx & 63u) ^ 32u) - 32;
+            const uint32_t idx = (kx >> 8) & 63u;
+            const bool real = (kx >> 14) & 1u;
+            const uint32_t dummy = rx_wb + rx_ent(lane, kRxDummyRow);
+            const int rows8 = 8 * S.rl;
+#pragma unroll
+            for (int j = 1; j <= 3; ++j) {
+                const int pw = 8 * j + kf - 1;
+                const bool w = real && pw >= 7 && pw <= 17 && 8 * j + col + 1 < rows8;
+                const uint32_t row = static_cast<uint32_t>(kRxHdrRows >> (4u * (static_cast<uint32_t>(pw - 7) & 15u))) & 15u;
+                *reinterpret_cast<uint32_t *>(rec + (w ? rx_wb + rx_ent(idx, row) : dummy)) = S.u[j];
+            }
+        }
+    };
+    // RX: the block's descriptors, decoded lane = packet in the record (rx_decode's fields; ok = the
+    // verify result in rbv; each row read before it is rewritten), then transposed on the way out:
+    // dword g = 64 t + lane of the block's 4608 bytes is dword g % 18 of packet g / 18.  The ok
+    // bytes (and, zero_trailer, the zeroed trailers) leave with them.
+    auto rx_block = [&](const OctSlot<MODE, TRAILER> &S) __attribute__((always_inline)) {
+        if constexpr (RX && D::kRxDecode) {
+            char *rec = const_cast<char *>(lds);
+            const uint32_t blk = S.rq & 0x7FFFFFFFu;
+            const bool mine = (S.rq >> 31) == 0u;
+            const uint32_t base = lo + blk * 64u;
+            const uint32_t cnt = nq - blk * 64u < 64u ? nq - blk * 64u : 64u;  // (strided: all of them this kernel's)
+            auto rd = [&](uint32_t r) __attribute__((always_inline)) { return lds_at(lds, rx_wb + rx_ent(lane, r)); };
+            auto wr = [&](uint32_t r, uint32_t v) __attribute__((always_inline)) {  // (sched_barrier: few live registers)
+                *reinterpret_cast<uint32_t *>(rec + rx_wb + rx_ent(lane, r)) = v;
+                if constexpr (D::kRxWrBarrier) __builtin_amdgcn_sched_barrier(0);
+            };
+            const uint32_t L = p.ulen;  // (strided batches)
+            // Per lane, one register: hs (bits 0-5), pad (8-9), status (16-17), and which fields
+            // the packet has (bits 24-28: ok, RETH, secondary RETH, immediate, AETH); the selects
+            // are bit-field masks, not lane masks (the ring leaves few SGPRs).
+            uint32_t meta;
+            {
+                const uint32_t w7 = rd(15);
+                const uint32_t op = w7 & 0x1Fu, tran = (w7 >> 5) & 7u, pad = (w7 >> 13) & 3u;
+                const uint32_t hs = (op == 0x09u || op == 0x0Bu) ? 32u
+                                  : (op == 0x0Cu)                 ? 44u
+                                  : (op == 0x11u)                 ? 16u
+                                  : (op >= 0x06u && op <= 0x10u)  ? 28u
+                                                                  : 0u;
+                const uint32_t status = (hs == 0u)           ? ICRC_RX_INVALID_OPCODE
+                                      : (tran > 6u)          ? ICRC_RX_INVALID_TRANS_TYPE
+                                      : (L - 32u < hs + pad) ? ICRC_RX_TRUNCATED
+                                                             : ICRC_RX_OK;  // (L >= 44: this kernel's packets)
+                const uint32_t okb = status == ICRC_RX_OK ? 1u : 0u;
+                const uint32_t cls = okb | (hs != 16u ? 2u : 16u) | (hs == 44u ? 4u : 0u) | (hs == 32u ? 8u : 0u);
+                meta = hs | (pad << 8) | (status << 16) | ((okb ? cls : 0u) << 24);
+            }
+            auto keep = [&](int bit, uint32_t v) __attribute__((always_inline)) {  // v if the packet has field `bit`
+                return v & static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(meta), 24 + bit, 1));
+            };
+            const uint32_t hs = meta & 63u, pad = (meta >> 8) & 3u;
+            {   // the dwords formed from words 7, 9, 10 first (rows 13-15 are rewritten here)
+                const uint32_t w7 = rd(15), w9 = rd(13), w10 = rd(14);
+                const uint32_t fl = (w7 >> 8) & 0xFFu;
+                const bool ack = hs == 16u;
+                const uint32_t flags = ((fl & 0x80u) ? ICRC_RX_SOLICITED : 0u) | ((w9 & 0x80u) ? ICRC_RX_ACK_REQ : 0u) |
+                                       (ack ? ICRC_RX_ACKNOWLEDGE : 0u) | (hs == 32u ? ICRC_RX_HAS_IMM : 0u) |
+                                       (hs == 44u ? ICRC_RX_HAS_SECONDARY_RETH : 0u);
+                const uint32_t code = ack ? (w10 >> 5) & 3u : 0u, value = ack ? w10 & 0x1Fu : 0u;
+                wr(16, keep(0, flags | (pad << 8) | (code << 16) | (value << 24)));
+                wr(1, keep(1, bswap32(w10)));                                   // RETH va high: word 10
+                wr(14, keep(4, bswap32(w10) & 0xFFFFFFu));                       // AETH msn
+                wr(13, keep(0, bswap32(w9) & 0xFFFFFFu));                        // psn
+                wr(15, keep(0, bswap16(w7 >> 16) | ((w7 & 0x1Fu) << 16) | (((w7 >> 5) & 7u) << 24)));  // pkey, opcode, transport
+            }
+            wr(17, (rbv & 0xFFu) | (meta & 0x30000u) >> 8);  // icrc_ok, status
+            wr(0, keep(1, bswap32(rd(0))));   // RETH va low: word 11
+            wr(2, keep(2, bswap32(rd(2))));   // secondary RETH va (bytes 56-63): words 15, 14
+            wr(3, keep(2, bswap32(rd(11))));
+            wr(11, keep(3, bswap32(rd(11))));  // immediate: word 14
+            wr(7, keep(1, bswap32(rd(7))));    // rkey, dlen: words 12, 13
+            wr(8, keep(1, bswap32(rd(8))));
+            wr(9, keep(2, bswap32(rd(9))));    // secondary rkey, dlen: words 16, 17
+            wr(10, keep(2, bswap32(rd(10))));
+            wr(12, keep(0, bswap32(rd(12)) & 0xFFFFFFu));  // dqpn: word 8
+            {
+                const uint64_t poff = static_cast<uint64_t>(base + lane) * p.stride + 28u + hs;
+                wr(4, keep(0, static_cast<uint32_t>(poff)));
+                wr(5, keep(0, static_cast<uint32_t>(poff >> 32)));
+            }
+            wr(6, keep(0, L - 32u - hs - pad));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint8_t *>(p.rx + base), 0, D::kRxStoreOOR ? 0 : static_cast<int>(cnt * 72u), 0x00020000);
+            if constexpr (D::kRxX4) {
+                // chunk c = 64 t + lane (16 bytes, dwords 4 c .. 4 c + 3 of the block) per store
+                uint32_t pk = (4u * lane * 3641u) >> 16, kk = 4u * lane - 18u * pk;  // 4 lane / 18, 4 lane % 18
+                asm volatile("" : "+v"(pk), "+v"(kk));
+#pragma clang loop unroll(disable)
+                for (uint32_t t = 0; t < 5; ++t) {
+                    u32x4 v;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        v[j] = lds_at(lds, rx_wb + rx_ent(pk, kk));
+                        ++kk;
+                        pk += kk == 18u ? 1u : 0u;
+                        kk = kk == 18u ? 0u : kk;
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>((64u * t + lane) * 16u), 0, D::kRxStoreAux);
+                    pk += 14u;  // + 256 dwords = 18 x 14 + 4 (the 4 stepped above)
+                }
+            } else {
+                uint32_t pk = (lane * 3641u) >> 16, kk = lane - 18u * pk;  // lane / 18 (exact below 64), lane % 18
+                // (opaque here: otherwise the 18 addresses, which depend on the lane alone, are hoisted out of
+                // the ring loop and held in 18 registers)
+                asm volatile("" : "+v"(pk), "+v"(kk));
+                // (a loop, not unrolled: this runs four times inlined in the ring, whose code already
+                // fills most of the instruction cache)
+#pragma clang loop unroll(disable)
+                for (uint32_t t = 0; t < 18; ++t) {
+                    const uint32_t v = lds_at(lds, rx_wb + rx_ent(pk, kk));
+                    __builtin_amdgcn_raw_buffer_store_b32(v, rs, static_cast<int>((64u * t + lane) * 4u), 0, D::kRxStoreAux);
+                    kk += 10u;  // g + 64 = 18 (pk + 3) + kk + 10
+                    pk += 3u;
+                    pk += kk >= 18u ? 1u : 0u;
+                    kk -= kk >= 18u ? 18u : 0u;
+                }
+            }
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
+                p.ok ? p.ok + lo : nullptr, 0, p.ok && !D::kRxStoreOOR ? static_cast<int>(nq) : 0, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rbv), os, static_cast<int>(mine ? blk * 64u + lane : kOctOOR), 0, 0);
+            if constexpr (TRAILER) {  // is_icrc_valid zeroes the trailer (stride <= 16 MiB: offsets below 1 GiB)
+                const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
+                    p.base + static_cast<uint64_t>(base) * p.stride, 0, static_cast<int>(kOctOOR), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    0u, ts, static_cast<int>(mine ? lane * static_cast<uint32_t>(p.stride) + L - 4u : kOctOOR), 0, 0);
+            }
+        }
     };
 
     // the result of a slot's set (its last frame): ICRC / verify result, routed into rbv
@@ -513,7 +716,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // around a store in the ring)
     auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
         if constexpr (!D::kStores) return;
-        if (TRAILER && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
+        if (TRAILER && !RX && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
                 __builtin_amdgcn_make_buffer_rsrc(p.base + S.boff, 0, static_cast<int>(kOctOOR), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(MODE == kCompute ? crc : 0u, ts, static_cast<int>(S.tro), 0, 0);
@@ -521,6 +724,10 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         // the block's results are complete after its last set: into the register buffer, which
         // is stored when full (and after the ring)
         if (!(S.fl & kOctBlockLast)) return;
+        if constexpr (RX) {  // the ok bytes leave with the block's descriptors (no result buffer)
+            rx_block(S);
+            return;
+        }
 #pragma unroll
         for (int e = 0; e + 1 < kOctRes; ++e) rres[e] = rres[e + 1];
         rres[kOctRes - 1] = rbv;
@@ -563,8 +770,12 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         inflight -= ((fa & kOctHave) ? 1 : 0) + ((fb & kOctHave) ? 1 : 0);
         // A's results (and its block's result store) before B's routing touches rbv: B may hold
         // the next block's first set
+        // (RX: a slot's words reach the record before its block's decode, and B's -- possibly the next
+        // block's first set -- only after A's decode)
+        deposit(SA);
         if (fa & kOctLast) finish(SA, crcA);
         stores(SA, crcA);
+        deposit(SB);
         if (fb & kOctLast) finish(SB, crcB);
         stores(SB, crcB);
     };
@@ -716,6 +927,45 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_self_kernel(Batc
     __syncthreads();  // every wave is done with the oct image before the long body rewrites LDS
     long_body<MODE, COMPACT, TRAILER>(p, lds4, blockIdx.x, gridDim.x);
 }
+// The fused receive of strided batches of short packets (icrc_rx_parse_device's default for them):
+// the oct verify on the receive kernel's LDS map (above run_oct): bulk entry (b, x) at row
+// (b >> 1) * 256 + x, the even table at slot (lane & 15) * 4, the odd one 64 bytes on (thread t
+// writes entry t's 16 copies as four 16-byte stores, the k-th at chunk (k + x) & 3).
+template <bool TRAILER, class D = OctProduct>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_rx_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    {   // thread t: bulk entry t's 16 copies (lower half of its table row) and 16 bytes of the final
+        // tables (row t >> 3, lanes 4 (t & 7) .. + 3 of the compact form's 64-lane rows)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(p.table_oct + kLdsWords), 0, static_cast<int>(kCompactWords * 4u), 0x00020000);
+        const uint32_t bulk = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(4u * threadIdx.x), 0, 0);
+        const uint32_t r = threadIdx.x >> 3, q = threadIdx.x & 7u;
+        const auto f = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(4096u + r * 256u + q * 16u), 0, 0);
+        const uint32_t b = threadIdx.x >> 8, x = threadIdx.x & 255u;
+        const uint32_t row = ((b >> 1) * 65536u + x * 256u + (b & 1u) * 64u) / 16u;
+        const uint4 v = make_uint4(bulk, bulk, bulk, bulk);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) lds4[row + ((k + x) & 3u)] = v;
+        lds4[(r * 256u + 128u + q * 16u) / 16u] = make_uint4(f[0], f[1], f[2], f[3]);
+        __syncthreads();
+    }
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    LaneConsts c;
+    c.pc = ((lane & 15u) * 4u) | (((lane & 15u) * 4u + 64u) << 8) | (1u << 16);
+    c.fin = 128u + (lane & 31u) * 4u;
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    uint32_t chunk = (p.n + tw - 1) / tw;
+    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 7u) & ~7u;
+    uint64_t lo64, hi64;
+    wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew & 0xFFFFu, lo64, hi64);
+    if (lo64 >= p.n) return;
+    const uint32_t lo = static_cast<uint32_t>(lo64);
+    const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
+    run_oct<kVerify, false, TRAILER, D, true>(p, lds, c, lane, lo, nq);
+}
+
 #ifdef ICRC_AB_BUILD
 // A/B (ICRC_AB_HYBRID_STAMP=1, compute): the hybrid kernel with each workgroup's start and end
 // (s_memrealtime, 100 MHz) and kind stored in g_hybrid_stamps, entry b = {start lo, start hi, end
@@ -797,6 +1047,29 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
 #undef ICRC_OD
 #endif
 #undef ICRC_O
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#ifdef ICRC_AB_BUILD
+    if (diag >= 2 && diag <= 8 && !p.trailer) {
+        switch (diag) {
+        case 2: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<2>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<3>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<4>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 5: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<5>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 6: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<6>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 7: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<7>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        default: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<8>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        }
+        return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+    }
+#else
+    (void)diag;
+#endif
+    if (p.trailer) hipLaunchKernelGGL((icrc_oct_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    else hipLaunchKernelGGL((icrc_oct_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

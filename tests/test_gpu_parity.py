@@ -838,6 +838,82 @@ def test_rx_parse_c1_stream(engine, ragged, rx_variant):
     assert np.all(got["payload_len"] == 4096) and np.all(got["status"] == 0)
 
 
+def _strided_rx_batch(L, n, stride, seed):
+    """n packets of exactly L bytes at `stride`: the header bytes of rx_cases' corpus (every opcode,
+    the corrupted opcode / transport / pad ones) round-robin, random bytes after them, the ICRC
+    written into each trailer, then every 29th trailer flipped."""
+    import rx_cases
+
+    rng = np.random.default_rng(seed)
+    corpus = [p for p in rx_cases.make_packets(rng) if p.size >= 44]
+    buf = rng.integers(0, 256, n * stride + 8, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    lens = np.full(n, L, np.uint32)
+    for i in range(n):
+        t = corpus[i % len(corpus)]
+        m = min(L - 4, t.size - 4)
+        buf[i * stride: i * stride + m] = t[:m]
+    ic = oracle.compute_icrc_batch(buf, off, lens)
+    tr = (off + np.uint64(L - 4)).astype(np.int64)
+    for k in range(4):
+        buf[tr + k] = ((ic >> (8 * k)) & 0xFF).astype(np.uint8)
+    buf[tr[::29]] ^= 0x40
+    return buf, off, lens
+
+
+@pytest.mark.parametrize("L", [44, 48, 60, 64, 72, 76, 316, 320, 652, 1084, 1088])
+@pytest.mark.parametrize("zero_trailer", [False, True])
+def test_rx_parse_strided_short_one_pass(engine, L, zero_trailer):
+    """Strided batches of short packets take ONE pass (icrc_oct_rx_kernel: the oct verify keeps
+    the header words it loads, words 7..17, and stores the descriptors itself): every opcode's
+    header and the corrupted ones at lengths from 44 B (the trailer inside word 10) to the oct
+    kernel's 1088, a batch above the one-pass small-batch boundary with a ragged last block, packed
+    and padded strides; descriptors, ok bytes and the zeroed trailers against the oracle, and the
+    same descriptors with no ok array."""
+    import icrc_amd
+
+    n = torch.cuda.get_device_properties(0).multi_processor_count * 16 * 3 + 37
+    stride = L if L % 8 else L + 12
+    buf, off, lens = _strided_rx_batch(L, n, stride, L * 2 + int(zero_trailer))
+    ref = buf.copy()
+    want = oracle.rx_parse(ref, off, lens, zero_trailer=zero_trailer)
+    for with_ok in (True, False):
+        d_buf = dev(buf)
+        d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+        d_ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        engine.rx_parse(d_buf.data_ptr(), 0, 0, n, d_desc.data_ptr(), d_ok.data_ptr() if with_ok else 0,
+                        zero_trailer=zero_trailer, stride=stride, length=L, stream=stream_handle())
+        torch.cuda.synchronize()
+        got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+        assert_desc_equal(got, want)
+        if with_ok:
+            np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
+        np.testing.assert_array_equal(d_buf.cpu().numpy(), ref)
+    assert int(np.sum(want["icrc_ok"] == 0)) >= (n + 28) // 29  # the flipped trailers (and the corpus' own)
+    assert len(set(want["status"].tolist())) >= 3  # ok, invalid opcode / transport, truncated
+    assert L < 76 or len(set(want["opcode"].tolist())) >= 12
+
+
+@pytest.mark.parametrize("L", [316, 1084])
+def test_rx_parse_strided_short_one_pass_full_blocks(engine, L):
+    """The one-pass receive over 300 000 packets: every wave owns whole 64-packet blocks (several
+    per wave, the per-wave LDS record reused block after block)."""
+    import icrc_amd
+
+    n = 300_000
+    buf, off, lens = _strided_rx_batch(L, n, L, 5 + L)
+    want = oracle.rx_parse(buf.copy(), off, lens)
+    d_buf = dev(buf)
+    d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.rx_parse(d_buf.data_ptr(), 0, 0, n, d_desc.data_ptr(), d_ok.data_ptr(), stride=L, length=L,
+                    stream=stream_handle())
+    torch.cuda.synchronize()
+    got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+    assert_desc_equal(got, want)
+    np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
+
+
 def test_send_receive_roundtrip(engine):
     """Packetize 24 WRITE / READ RESPONSE messages on the GPU, parse them on the GPU, and place each
     payload at its RETH va: the memory region equals the source bytes (C3 closed on-device)."""
