@@ -323,6 +323,7 @@ struct OctProduct {
     static constexpr bool kRxWrBarrier = true; // RX: a scheduling barrier after each record write of the decode
     static constexpr bool kRxX4 = false;       // RX: the descriptors leave as 16-byte stores (else dword stores)
     static constexpr int kRxStoreAux = kStreamAux;  // RX: the descriptor stores' cache policy (nt: -2.5 %, rx_oct_ab)
+    static constexpr bool kRxDefer = false;    // RX: the descriptor stores after the next pair's loads
 };
 #ifdef ICRC_AB_BUILD
 // 41 loads only; 42 row steps, no loads; 43 control and final products; 44 control only; 45 = 41
@@ -345,13 +346,14 @@ struct OctAblation : OctProduct {
 // The receive kernel's cuts and alternatives (ICRC_AB_RX_OCT=2..8): 2 no record writes, 3 no block
 // decode / stores, 4 neither (the 16-copy verify alone), 5 the decode with every global store out
 // of range; 6 the descriptor stores without the non-temporal hint, 7 (= the product), 8 16-byte
-// non-temporal descriptor stores.
+// non-temporal descriptor stores; 9 the descriptor stores deferred past the next pair's loads.
 template <int X>
 struct OctRxAblation : OctProduct {
     static constexpr bool kRxDeposit = !(X == 2 || X == 4);
     static constexpr bool kRxDecode = !(X == 3 || X == 4);
     static constexpr bool kRxStoreOOR = X == 5;
     static constexpr bool kRxX4 = X == 8;
+    static constexpr bool kRxDefer = X == 9;
     static constexpr int kRxStoreAux = (X == 6 || X == 5) ? 0 : kStreamAux;
 };
 #endif
@@ -589,7 +591,49 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // verify result in rbv; each row read before it is rewritten), then transposed on the way out:
     // dword g = 64 t + lane of the block's 4608 bytes is dword g % 18 of packet g / 18.  The ok
     // bytes (and, zero_trailer, the zeroed trailers) leave with them.
-    auto rx_block = [&](const OctSlot<MODE, TRAILER> &S) __attribute__((always_inline)) {
+    // RX: the read-back of a decoded block (packets base .. base + cnt - 1): dword g = 64 t + lane of
+    // its 4608 bytes is dword g % 18 of packet g / 18; 18 coalesced stores.
+    uint32_t rx_pbase = 0, rx_pcnt = 0;
+    bool rx_pend = false;
+    auto rx_readback = [&](uint32_t base, uint32_t cnt) __attribute__((always_inline)) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<uint8_t *>(p.rx + base), 0, D::kRxStoreOOR ? 0 : static_cast<int>(cnt * 72u), 0x00020000);
+        if constexpr (D::kRxX4) {
+            // chunk c = 64 t + lane (16 bytes, dwords 4 c .. 4 c + 3 of the block) per store
+            uint32_t pk = (4u * lane * 3641u) >> 16, kk = 4u * lane - 18u * pk;  // 4 lane / 18, 4 lane % 18
+            asm volatile("" : "+v"(pk), "+v"(kk));
+#pragma clang loop unroll(disable)
+            for (uint32_t t = 0; t < 5; ++t) {
+                u32x4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[j] = lds_at(lds, rx_wb + rx_ent(pk, kk));
+                    ++kk;
+                    pk += kk == 18u ? 1u : 0u;
+                    kk = kk == 18u ? 0u : kk;
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>((64u * t + lane) * 16u), 0, D::kRxStoreAux);
+                pk += 14u;  // + 256 dwords = 18 x 14 + 4 (the 4 stepped above)
+            }
+        } else {
+            uint32_t pk = (lane * 3641u) >> 16, kk = lane - 18u * pk;  // lane / 18 (exact below 64), lane % 18
+            // (opaque here: otherwise the 18 addresses, which depend on the lane alone, are hoisted out of
+            // the ring loop and held in 18 registers)
+            asm volatile("" : "+v"(pk), "+v"(kk));
+            // (a loop, not unrolled: this runs four times inlined in the ring, whose code already
+            // fills most of the instruction cache)
+#pragma clang loop unroll(disable)
+            for (uint32_t t = 0; t < 18; ++t) {
+                const uint32_t v = lds_at(lds, rx_wb + rx_ent(pk, kk));
+                __builtin_amdgcn_raw_buffer_store_b32(v, rs, static_cast<int>((64u * t + lane) * 4u), 0, D::kRxStoreAux);
+                kk += 10u;  // g + 64 = 18 (pk + 3) + kk + 10
+                pk += 3u;
+                pk += kk >= 18u ? 1u : 0u;
+                kk -= kk >= 18u ? 18u : 0u;
+            }
+        }
+    };
+    auto rx_block = [&](const OctSlot<MODE, TRAILER> &S, bool can_defer) __attribute__((always_inline)) {
         if constexpr (RX && D::kRxDecode) {
             char *rec = const_cast<char *>(lds);
             const uint32_t blk = S.rq & 0x7FFFFFFFu;
@@ -656,42 +700,6 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 wr(5, keep(0, static_cast<uint32_t>(poff >> 32)));
             }
             wr(6, keep(0, L - 32u - hs - pad));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<uint8_t *>(p.rx + base), 0, D::kRxStoreOOR ? 0 : static_cast<int>(cnt * 72u), 0x00020000);
-            if constexpr (D::kRxX4) {
-                // chunk c = 64 t + lane (16 bytes, dwords 4 c .. 4 c + 3 of the block) per store
-                uint32_t pk = (4u * lane * 3641u) >> 16, kk = 4u * lane - 18u * pk;  // 4 lane / 18, 4 lane % 18
-                asm volatile("" : "+v"(pk), "+v"(kk));
-#pragma clang loop unroll(disable)
-                for (uint32_t t = 0; t < 5; ++t) {
-                    u32x4 v;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        v[j] = lds_at(lds, rx_wb + rx_ent(pk, kk));
-                        ++kk;
-                        pk += kk == 18u ? 1u : 0u;
-                        kk = kk == 18u ? 0u : kk;
-                    }
-                    __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>((64u * t + lane) * 16u), 0, D::kRxStoreAux);
-                    pk += 14u;  // + 256 dwords = 18 x 14 + 4 (the 4 stepped above)
-                }
-            } else {
-                uint32_t pk = (lane * 3641u) >> 16, kk = lane - 18u * pk;  // lane / 18 (exact below 64), lane % 18
-                // (opaque here: otherwise the 18 addresses, which depend on the lane alone, are hoisted out of
-                // the ring loop and held in 18 registers)
-                asm volatile("" : "+v"(pk), "+v"(kk));
-                // (a loop, not unrolled: this runs four times inlined in the ring, whose code already
-                // fills most of the instruction cache)
-#pragma clang loop unroll(disable)
-                for (uint32_t t = 0; t < 18; ++t) {
-                    const uint32_t v = lds_at(lds, rx_wb + rx_ent(pk, kk));
-                    __builtin_amdgcn_raw_buffer_store_b32(v, rs, static_cast<int>((64u * t + lane) * 4u), 0, D::kRxStoreAux);
-                    kk += 10u;  // g + 64 = 18 (pk + 3) + kk + 10
-                    pk += 3u;
-                    pk += kk >= 18u ? 1u : 0u;
-                    kk -= kk >= 18u ? 18u : 0u;
-                }
-            }
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
                 p.ok ? p.ok + lo : nullptr, 0, p.ok && !D::kRxStoreOOR ? static_cast<int>(nq) : 0, 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rbv), os, static_cast<int>(mine ? blk * 64u + lane : kOctOOR), 0, 0);
@@ -700,6 +708,17 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                     p.base + static_cast<uint64_t>(base) * p.stride, 0, static_cast<int>(kOctOOR), 0x00020000);
                 __builtin_amdgcn_raw_buffer_store_b32(
                     0u, ts, static_cast<int>(mine ? lane * static_cast<uint32_t>(p.stride) + L - 4u : kOctOOR), 0, 0);
+            }
+            // The descriptor stores now, or (D::kRxDefer) at the start of the next consume, after the
+            // next pair's loads: a store sits in the load queue, and there it must complete one ring
+            // step later instead of at the next wait.  Deferred only when no deposit follows in this
+            // consume (the record is read back before it is rewritten).
+            if (D::kRxDefer && can_defer) {
+                rx_pend = true;
+                rx_pbase = base;
+                rx_pcnt = cnt;
+            } else {
+                rx_readback(base, cnt);
             }
         }
     };
@@ -714,7 +733,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     };
     // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
     // around a store in the ring)
-    auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc) __attribute__((always_inline)) {
+    auto stores = [&](const OctSlot<MODE, TRAILER> &S, uint32_t crc, bool can_defer) __attribute__((always_inline)) {
         if constexpr (!D::kStores) return;
         if (TRAILER && !RX && (S.fl & kOctLast)) {  // PacketWriter stores the ICRC / is_icrc_valid zeroes it
             const __amdgpu_buffer_rsrc_t ts =
@@ -725,7 +744,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         // is stored when full (and after the ring)
         if (!(S.fl & kOctBlockLast)) return;
         if constexpr (RX) {  // the ok bytes leave with the block's descriptors (no result buffer)
-            rx_block(S);
+            rx_block(S, can_defer);
             return;
         }
 #pragma unroll
@@ -745,6 +764,12 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     // independent and, when both are full and uniform, stepped interleaved.
     auto consume = [&](auto ac) __attribute__((always_inline)) {
         constexpr int a = decltype(ac)::value;
+        if constexpr (RX && D::kRxDefer) {
+            if (rx_pend) {
+                rx_readback(rx_pbase, rx_pcnt);
+                rx_pend = false;
+            }
+        }
         OctSlot<MODE, TRAILER> &SA = sl[a];
         OctSlot<MODE, TRAILER> &SB = sl[a + 1];
         const uint32_t fa = SA.fl, fb = SB.fl;
@@ -774,10 +799,10 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         // block's first set -- only after A's decode)
         deposit(SA);
         if (fa & kOctLast) finish(SA, crcA);
-        stores(SA, crcA);
+        stores(SA, crcA, !(fb & kOctFirst));
         deposit(SB);
         if (fb & kOctLast) finish(SB, crcB);
-        stores(SB, crcB);
+        stores(SB, crcB, true);
     };
 
     int cycles = 0;
@@ -834,6 +859,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         }
     }
     if (nres) flush();
+    if (RX && rx_pend) rx_readback(rx_pbase, rx_pcnt);
     if (bailed) {  // never reached by correct bookkeeping: make it loud, not silent
         for (uint32_t i = lane; i < nq; i += 64u) store_result<MODE>(p, lo + i, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN);
         if (p.nerr && lane == 0) atomicAdd(p.nerr, nq);
@@ -1053,7 +1079,7 @@ int launch_oct(int mode, const BatchParams &p, int grid, void *stream, int diag)
 int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag) {
     hipStream_t s = static_cast<hipStream_t>(stream);
 #ifdef ICRC_AB_BUILD
-    if (diag >= 2 && diag <= 8 && !p.trailer) {
+    if (diag >= 2 && diag <= 9 && !p.trailer) {
         switch (diag) {
         case 2: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<2>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
         case 3: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<3>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
@@ -1061,7 +1087,8 @@ int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag) {
         case 5: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<5>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
         case 6: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<6>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
         case 7: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<7>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-        default: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<8>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        case 8: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<8>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+        default: hipLaunchKernelGGL((icrc_oct_rx_kernel<false, OctRxAblation<9>>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
         }
         return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
     }

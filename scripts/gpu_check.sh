@@ -26,7 +26,7 @@ if [ "${PROFILE:-1}" = 1 ]; then
   echo "== rocprofv3"
   rm -rf $OUT/prof
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-    python3 bench.py --no-cpu > $OUT/prof.log 2>&1; rc=$?
+    python3 bench.py --no-cpu ${PROFILE_ARGS:-} > $OUT/prof.log 2>&1; rc=$?
   tail -3 $OUT/prof.log; stop_if_fatal $rc rocprof
   find $OUT/prof -name "*kernel_stats.csv" -exec cat {} \;
 fi
