@@ -222,7 +222,14 @@ struct OctSlot {
 // The row steps of one frame.  FIRST: rows 0..2 carry the header masks and row 0 starts the
 // accumulators; UNI: no per-lane freeze; FULL: all K rows (else rows past S.rrem are skipped, a
 // uniform branch per row).
-template <bool FIRST, bool UNI, bool FULL, int MODE, bool TRAILER>
+// A slot's rows from its row 0 (the freeze count): OctSlot::rl, or (PK, the receive kernel) bits
+// 16-23 of OctSlot::kf, signed -- one register fewer per slot.
+template <bool PK, int MODE, bool TRAILER>
+__device__ __forceinline__ int slot_rows(const OctSlot<MODE, TRAILER> &S) {
+    return PK ? __builtin_amdgcn_sbfe(S.kf, 16, 8) : S.rl;
+}
+
+template <bool FIRST, bool UNI, bool FULL, int MODE, bool TRAILER, bool PK = false>
 __device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm,
                                              const char *lds, const LaneConsts &c) {
     uint32_t m0 = 0, m1 = 0, m2 = 0;
@@ -243,13 +250,13 @@ __device__ __forceinline__ uint32_t oct_rows(const OctSlot<MODE, TRAILER> &S, ui
         }
         const uint32_t nv = (FIRST && j == 0) ? u : step_m64(lds, acc, u, c);
         if constexpr (UNI) acc = nv;
-        else acc = j < S.rl ? nv : acc;
+        else acc = j < slot_rows<PK>(S) ? nv : acc;
     }
     return acc;
 }
 
 // One frame's rows, dispatched on its (uniform) flags.
-template <int MODE, bool TRAILER, class D>
+template <int MODE, bool TRAILER, class D, bool PK = false>
 __device__ __forceinline__ uint32_t oct_frame(const OctSlot<MODE, TRAILER> &S, uint32_t acc, uint32_t hm, const char *lds,
                                               const LaneConsts &c) {
     if constexpr (!D::kRows) {
@@ -258,13 +265,13 @@ __device__ __forceinline__ uint32_t oct_frame(const OctSlot<MODE, TRAILER> &S, u
         return acc;
     } else {
         switch (S.fl & (kOctFirst | kOctUni | kOctFull)) {
-        case kOctFirst | kOctUni | kOctFull: return oct_rows<true, true, true>(S, acc, hm, lds, c);
-        case kOctFirst | kOctFull: return oct_rows<true, false, true>(S, acc, hm, lds, c);
-        case kOctUni | kOctFull: return oct_rows<false, true, true>(S, acc, hm, lds, c);
-        case kOctFull: return oct_rows<false, false, true>(S, acc, hm, lds, c);
+        case kOctFirst | kOctUni | kOctFull: return oct_rows<true, true, true, MODE, TRAILER, PK>(S, acc, hm, lds, c);
+        case kOctFirst | kOctFull: return oct_rows<true, false, true, MODE, TRAILER, PK>(S, acc, hm, lds, c);
+        case kOctUni | kOctFull: return oct_rows<false, true, true, MODE, TRAILER, PK>(S, acc, hm, lds, c);
+        case kOctFull: return oct_rows<false, false, true, MODE, TRAILER, PK>(S, acc, hm, lds, c);
         case kOctFirst | kOctUni:
-        case kOctFirst: return oct_rows<true, false, false>(S, acc, hm, lds, c);
-        default: return oct_rows<false, false, false>(S, acc, hm, lds, c);
+        case kOctFirst: return oct_rows<true, false, false, MODE, TRAILER, PK>(S, acc, hm, lds, c);
+        default: return oct_rows<false, false, false, MODE, TRAILER, PK>(S, acc, hm, lds, c);
         }
     }
 }
@@ -376,7 +383,10 @@ struct OctRxAblation : OctProduct {
 // rows 128..507, waves 10..15 two by two in the old final-table region.  Row k = dword k of the
 // packets' descriptors; before the decode, header word w sits in the row of the dword formed from
 // it (kRxHdrRows), so the decode reads and writes each row in place; row 18 takes a deposit lane's
-// unused writes.  One record per wave: a block's words are written when its sets' first frames are
+// unused writes (entries 0..31) and, ragged batches, the base offsets of the wave's last eight
+// prepared blocks (entries 32..47, written when a block is prepared, read by its decode; at most
+// six blocks lie between the two).  Ragged batches also deposit each packet's offset from its
+// block's base and its length into rows 4 and 6 (dwords computed from them, rewritten last).  One record per wave: a block's words are written when its sets' first frames are
 // consumed, decoded and stored when its last frame is, and the next block's first frame is
 // consumed after that (consume orders deposit / finish / stores per slot).
 constexpr uint32_t kRxRows = 19u, kRxRecRow = 512u, kRxDummyRow = 18u;
@@ -391,13 +401,20 @@ __device__ __forceinline__ uint32_t rx_wave_base(uint32_t w) {
 // Packet i of record row k, rotated by 2 k within its 32-packet half: the decode (lane = packet, one
 // row) reads 32 banks either way, and the transposing read-back -- whose 32 lanes take ~18 rows of
 // two packets -- hits ~2 lanes per bank instead of ~18 (68 LDS cycles over its 18 reads against 640).
+// v, opaque to the optimiser: values derived from it inside the ring loop are recomputed there
+// instead of being hoisted out of it and held (the receive ring has no registers to spare: a held
+// lane constant spills, and a reload in the ring waits for every load before it).
+__device__ __forceinline__ uint32_t rx_opaque(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 __device__ __forceinline__ uint32_t rx_ent(uint32_t i, uint32_t k) {
     return k * kRxRecRow + ((i >> 5) << 8) + (((i + 2u * k) & 31u) << 2);
 }
 
 template <int MODE, bool RAGGED, bool TRAILER, class D, bool RX = false>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
-                                        uint32_t lo, uint32_t nq) {
+                                        uint32_t lo, uint32_t nq, bool *rx_rest = nullptr) {
     constexpr bool kPrio = kOctPrio && D::kPrio;
     constexpr int K = kOctK;
     constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
@@ -432,6 +449,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     int inflight = 0;
     // RX: the wave's record
     const uint32_t rx_wb = RX ? rx_wave_base(readfirstlane_u32(threadIdx.x >> 6)) : 0u;
+    const uint32_t lane_ = lane;  // (the block preparation's lane, opaque there under RX)
 
     OctSlot<MODE, TRAILER> sl[B];
 #pragma unroll
@@ -547,10 +565,17 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         }
         const bool last = (fd & kOctLast) != 0u;
-        // (RX: the packet's block index in bits 8-13, bit 14 set for a real packet; readers mask & 63)
-        S.kf = RX ? static_cast<int>((static_cast<uint32_t>(lkf) & 63u) | (lidx << 8)) : lkf;
-        S.rl = lr - K * static_cast<int>(lf);
+        // (RX: the packet's block index in bits 8-13, bit 14 set for a real packet, the rows from this
+        // frame's row 0 in bits 16-23 (slot_rows); readers mask & 63)
+        if constexpr (RX) {
+            const uint32_t rl = static_cast<uint32_t>(lr - K * static_cast<int>(lf)) & 0xFFu;
+            S.kf = static_cast<int>((static_cast<uint32_t>(lkf) & 63u) | (lidx << 8) | (rl << 16));
+        } else {
+            S.kf = lkf;
+            S.rl = lr - K * static_cast<int>(lf);
+        }
         if constexpr (!RX) S.tro = last ? ltr : kOctOOR;  // (RX: the block's trailers are zeroed with its descriptors)
+        else if constexpr (RAGGED) S.tro = lvrow0 + 4u - 4u * static_cast<uint32_t>(lkf);  // RX: the packet's offset from boff
         // routing: packet i of the block (pos_i = its sorted position, 0xFF if not this kernel's)
         // takes group (pos_i & 7)'s result at the last frame of set pos_i >> 3
         const uint32_t pi = LB.pos;
@@ -576,8 +601,9 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             const int kf = static_cast<int>((kx & 63u) ^ 32u) - 32;
             const uint32_t idx = (kx >> 8) & 63u;
             const bool real = (kx >> 14) & 1u;
-            const uint32_t dummy = rx_wb + rx_ent(lane, kRxDummyRow);
-            const int rows8 = 8 * S.rl;
+            const uint32_t ln = rx_opaque(lane);
+            const uint32_t dummy = rx_wb + rx_ent(ln & 31u, kRxDummyRow);
+            const int rows8 = 8 * slot_rows<true>(S);
 #pragma unroll
             for (int j = 1; j <= 3; ++j) {
                 const int pw = 8 * j + kf - 1;
@@ -585,10 +611,15 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 const uint32_t row = static_cast<uint32_t>(kRxHdrRows >> (4u * (static_cast<uint32_t>(pw - 7) & 15u))) & 15u;
                 *reinterpret_cast<uint32_t *>(rec + (w ? rx_wb + rx_ent(idx, row) : dummy)) = S.u[j];
             }
+            if constexpr (RAGGED) {  // lane 8 g: the offset from boff (row 4); 8 g + 1: L = 4 (N - 1), N = 8 R - c + kf
+                const uint32_t Lp = 4u * static_cast<uint32_t>(rows8 - col + kf) - 4u;
+                const bool w = real && col < 2;
+                *reinterpret_cast<uint32_t *>(rec + (w ? rx_wb + rx_ent(idx, col == 0 ? 4u : 6u) : dummy)) = col == 0 ? S.tro : Lp;
+            }
         }
     };
     // RX: the block's descriptors, decoded lane = packet in the record (rx_decode's fields; ok = the
-    // verify result in rbv; each row read before it is rewritten), then transposed on the way out:
+    // verify result finish left in row 17; each row read before it is rewritten), then transposed on the way out:
     // dword g = 64 t + lane of the block's 4608 bytes is dword g % 18 of packet g / 18.  The ok
     // bytes (and, zero_trailer, the zeroed trailers) leave with them.
     // RX: the read-back of a decoded block (packets base .. base + cnt - 1): dword g = 64 t + lane of
@@ -640,12 +671,14 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             const bool mine = (S.rq >> 31) == 0u;
             const uint32_t base = lo + blk * 64u;
             const uint32_t cnt = nq - blk * 64u < 64u ? nq - blk * 64u : 64u;  // (strided: all of them this kernel's)
-            auto rd = [&](uint32_t r) __attribute__((always_inline)) { return lds_at(lds, rx_wb + rx_ent(lane, r)); };
+            const uint32_t ln = rx_opaque(lane);
+            auto rd = [&](uint32_t r) __attribute__((always_inline)) { return lds_at(lds, rx_wb + rx_ent(ln, r)); };
             auto wr = [&](uint32_t r, uint32_t v) __attribute__((always_inline)) {  // (sched_barrier: few live registers)
-                *reinterpret_cast<uint32_t *>(rec + rx_wb + rx_ent(lane, r)) = v;
+                *reinterpret_cast<uint32_t *>(rec + rx_wb + rx_ent(ln, r)) = v;
                 if constexpr (D::kRxWrBarrier) __builtin_amdgcn_sched_barrier(0);
             };
-            const uint32_t L = p.ulen;  // (strided batches)
+            // the packet's length (ragged: record row 6, read again where needed: short live ranges)
+            auto len = [&]() __attribute__((always_inline)) { return RAGGED ? rd(6) : p.ulen; };
             // Per lane, one register: hs (bits 0-5), pad (8-9), status (16-17), and which fields
             // the packet has (bits 24-28: ok, RETH, secondary RETH, immediate, AETH); the selects
             // are bit-field masks, not lane masks (the ring leaves few SGPRs).
@@ -660,8 +693,8 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                                                                   : 0u;
                 const uint32_t status = (hs == 0u)           ? ICRC_RX_INVALID_OPCODE
                                       : (tran > 6u)          ? ICRC_RX_INVALID_TRANS_TYPE
-                                      : (L - 32u < hs + pad) ? ICRC_RX_TRUNCATED
-                                                             : ICRC_RX_OK;  // (L >= 44: this kernel's packets)
+                                      : (len() - 32u < hs + pad) ? ICRC_RX_TRUNCATED
+                                                                 : ICRC_RX_OK;  // (L >= 44: this kernel's packets)
                 const uint32_t okb = status == ICRC_RX_OK ? 1u : 0u;
                 const uint32_t cls = okb | (hs != 16u ? 2u : 16u) | (hs == 44u ? 4u : 0u) | (hs == 32u ? 8u : 0u);
                 meta = hs | (pad << 8) | (status << 16) | ((okb ? cls : 0u) << 24);
@@ -684,7 +717,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 wr(13, keep(0, bswap32(w9) & 0xFFFFFFu));                        // psn
                 wr(15, keep(0, bswap16(w7 >> 16) | ((w7 & 0x1Fu) << 16) | (((w7 >> 5) & 7u) << 24)));  // pkey, opcode, transport
             }
-            wr(17, (rbv & 0xFFu) | (meta & 0x30000u) >> 8);  // icrc_ok, status
+            wr(17, (rd(17) & 0xFFu) | (meta & 0x30000u) >> 8);  // icrc_ok (finish left it there), status
             wr(0, keep(1, bswap32(rd(0))));   // RETH va low: word 11
             wr(2, keep(2, bswap32(rd(2))));   // secondary RETH va (bytes 56-63): words 15, 14
             wr(3, keep(2, bswap32(rd(11))));
@@ -694,21 +727,27 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             wr(9, keep(2, bswap32(rd(9))));    // secondary rkey, dlen: words 16, 17
             wr(10, keep(2, bswap32(rd(10))));
             wr(12, keep(0, bswap32(rd(12)) & 0xFFFFFFu));  // dqpn: word 8
+            uint64_t boff = 0;  // ragged: the block's base offset (the ring in row 18) + record row 4
+            if constexpr (RAGGED) {
+                const uint32_t e = rx_wb + rx_ent(32u + 2u * (blk & 7u), kRxDummyRow);
+                boff = static_cast<uint64_t>(readfirstlane_u32(lds_at(lds, e))) |
+                       (static_cast<uint64_t>(readfirstlane_u32(lds_at(lds, e + 4u))) << 32);
+            }
+            if constexpr (TRAILER) {  // is_icrc_valid zeroes the trailer (strided: stride <= 16 MiB, offsets below 1 GiB)
+                const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
+                    p.base + (RAGGED ? boff : static_cast<uint64_t>(base) * p.stride), 0, static_cast<int>(kOctOOR), 0x00020000);
+                const uint32_t to = (RAGGED ? rd(4) : ln * static_cast<uint32_t>(p.stride)) + len() - 4u;
+                __builtin_amdgcn_raw_buffer_store_b32(0u, ts, static_cast<int>(mine ? to : kOctOOR), 0, 0);
+            }
+            wr(6, keep(0, len() - 32u - hs - pad));  // (ragged: row 6 held L until here)
             {
-                const uint64_t poff = static_cast<uint64_t>(base + lane) * p.stride + 28u + hs;
+                const uint64_t poff = (RAGGED ? boff + rd(4) : static_cast<uint64_t>(base + ln) * p.stride) + 28u + hs;
                 wr(4, keep(0, static_cast<uint32_t>(poff)));
                 wr(5, keep(0, static_cast<uint32_t>(poff >> 32)));
             }
-            wr(6, keep(0, L - 32u - hs - pad));
             const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(
                 p.ok ? p.ok + lo : nullptr, 0, p.ok && !D::kRxStoreOOR ? static_cast<int>(nq) : 0, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rbv), os, static_cast<int>(mine ? blk * 64u + lane : kOctOOR), 0, 0);
-            if constexpr (TRAILER) {  // is_icrc_valid zeroes the trailer (stride <= 16 MiB: offsets below 1 GiB)
-                const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
-                    p.base + static_cast<uint64_t>(base) * p.stride, 0, static_cast<int>(kOctOOR), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    0u, ts, static_cast<int>(mine ? lane * static_cast<uint32_t>(p.stride) + L - 4u : kOctOOR), 0, 0);
-            }
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(rd(17)), os, static_cast<int>(mine ? blk * 64u + ln : kOctOOR), 0, 0);
             // The descriptor stores now, or (D::kRxDefer) at the start of the next consume, after the
             // next pair's loads: a store sits in the load queue, and there it must complete one ring
             // step later instead of at the next wait.  Deferred only when no deposit follows in this
@@ -728,8 +767,15 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
         uint32_t r;
         if constexpr (MODE == kCompute) r = crc;
         else r = crc == kIcrcResidue ? ICRC_VERIFY_OK : ICRC_VERIFY_MISMATCH;  // over the trailer too
-        const uint32_t v = bperm(S.rt & 63u, r);
-        rbv = S.rt != 0xFFu ? v : rbv;
+        if constexpr (RX) {  // lane 8 g: into record row 17 of its packet (the block's decode reads it there)
+            const uint32_t kx = static_cast<uint32_t>(S.kf);
+            const bool w = ((kx >> 14) & 1u) && col == 0;
+            const uint32_t a = rx_wb + (w ? rx_ent((kx >> 8) & 63u, 17u) : rx_ent(rx_opaque(lane) & 31u, kRxDummyRow));
+            *reinterpret_cast<uint32_t *>(const_cast<char *>(lds) + a) = r;
+        } else {
+            const uint32_t v = bperm(S.rt & 63u, r);
+            rbv = S.rt != 0xFFu ? v : rbv;
+        }
     };
     // a slot's stores, issued whether or not it holds a frame (out of range otherwise: no branch
     // around a store in the ring)
@@ -779,8 +825,8 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             if (fa & kOctFirst) oct_rows2<true>(SA, SB, accA, accB, hm, lds, c);
             else oct_rows2<false>(SA, SB, accA, accB, hm, lds, c);
         } else {
-            if (fa & kOctHave) accA = oct_frame<MODE, TRAILER, D>(SA, accA, hm, lds, c);
-            if (fb & kOctHave) accB = oct_frame<MODE, TRAILER, D>(SB, (fb & kOctFirst) ? 0u : accA, hm, lds, c);
+            if (fa & kOctHave) accA = oct_frame<MODE, TRAILER, D, RX>(SA, accA, hm, lds, c);
+            if (fb & kOctHave) accB = oct_frame<MODE, TRAILER, D, RX>(SB, (fb & kOctFirst) ? 0u : accA, hm, lds, c);
         }
         acc_c = (fb & kOctHave) ? accB : accA;
         uint32_t crcA = 0, crcB = 0;
@@ -810,6 +856,7 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     for (;;) {
         // top of the cycle: prepare the next block, then fetch the (offset, len) of the one after
         if (!nb_ready && nb_next < nblocks && (!RAGGED || mblk == nb_next)) {
+            const uint32_t lane = RX ? rx_opaque(lane_) : lane_;  // (RX: rx_opaque)
             const uint32_t q = static_cast<uint32_t>(nb_next) * 64u + lane;
             const bool valid = q < nq;
             uint64_t off = 0;
@@ -826,6 +873,15 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
                 NB.boff = static_cast<uint64_t>(lo + static_cast<uint32_t>(nb_next) * 64u) * p.stride;
             } else if (oct_block<MODE>(p, NB, off, L, valid, lo, nb_next, lane) != 0) {
                 irregular = true;
+            }
+            if constexpr (RX && RAGGED) {
+                // packets left for the sweep (not this ring's: long, irregular)?
+                if (rx_rest && (__ballot(valid) & ~NB.mine) != 0ull) *rx_rest = true;
+            }
+            if constexpr (RX && RAGGED) {  // the block's base offset into the record's ring (row 18, entries 32..47)
+                const uint32_t e = rx_wb + rx_ent(32u + 2u * (static_cast<uint32_t>(nb_next) & 7u) + (lane & 1u), kRxDummyRow);
+                const uint32_t v = (lane & 1u) ? static_cast<uint32_t>(NB.boff >> 32) : static_cast<uint32_t>(NB.boff);
+                if (lane < 2u) *reinterpret_cast<uint32_t *>(const_cast<char *>(lds) + e) = v;
             }
             nb_next += 1;
             nb_ready = NB.nfr > 0;
@@ -957,9 +1013,11 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_self_kernel(Batc
 // the oct verify on the receive kernel's LDS map (above run_oct): bulk entry (b, x) at row
 // (b >> 1) * 256 + x, the even table at slot (lane & 15) * 4, the odd one 64 bytes on (thread t
 // writes entry t's 16 copies as four 16-byte stores, the k-th at chunk (k + x) & 3).
-template <bool TRAILER, class D = OctProduct>
-__global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_rx_kernel(BatchParams p) {
-    __shared__ uint4 lds4[kLdsBytes / 16];
+// The oct half of a receive kernel on workgroup blockIdx.x: the receive image, then run_oct (RX) on
+// this wave's range [lo, lo + nq); false if the wave has no range.
+template <bool TRAILER, class D, bool RAGGED>
+__device__ __forceinline__ bool rx_oct_part(const BatchParams &p, uint4 *lds4, uint32_t &lo, uint32_t &nq,
+                                            bool *rest = nullptr) {
     {   // thread t: bulk entry t's 16 copies (lower half of its table row) and 16 bytes of the final
         // tables (row t >> 3, lanes 4 (t & 7) .. + 3 of the compact form's 64-lane rows)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -986,10 +1044,78 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_rx_kernel(BatchPara
     chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 7u) & ~7u;
     uint64_t lo64, hi64;
     wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew & 0xFFFFu, lo64, hi64);
-    if (lo64 >= p.n) return;
-    const uint32_t lo = static_cast<uint32_t>(lo64);
-    const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
-    run_oct<kVerify, false, TRAILER, D, true>(p, lds, c, lane, lo, nq);
+    if (lo64 >= p.n) return false;
+    lo = static_cast<uint32_t>(lo64);
+    nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
+    run_oct<kVerify, RAGGED, TRAILER, D, true>(p, lds, c, lane, lo, nq, rest);
+    return true;
+}
+
+template <bool TRAILER, class D = OctProduct>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_rx_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    uint32_t lo, nq;
+    rx_oct_part<TRAILER, D, false>(p, lds4, lo, nq);
+}
+
+// The ragged one-pass receive: the packets the oct ring decoded keep their descriptors; the rest of
+// the wave's range (L >= split_len: verified by long_body; L < 44, misaligned, far apart: the oct
+// tail loop) are decoded here, lane = packet, from their header words and the ok bytes those paths
+// left in p.ok (a workgroup barrier before this: the long-packet waves are other waves of the same
+// workgroup, on the same workgroup range).  Their descriptors are stored lane = packet, outside any
+// load ring.
+__device__ __forceinline__ void rx_sweep(const BatchParams &p, uint32_t lo, uint32_t nq, uint32_t lane) {
+    __builtin_amdgcn_s_waitcnt(0);  // the ring's descriptor stores (garbage for these packets) land first
+    const int nblocks = static_cast<int>((nq + 63u) >> 6);
+    for (int b = 0; b < nblocks; ++b) {
+        const uint32_t q = static_cast<uint32_t>(b) * 64u + lane;
+        const bool valid = q < nq;
+        const uint32_t i = lo + q;
+        const uint64_t off = valid ? (p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride) : 0u;
+        const uint32_t L = valid ? (p.len ? p.len[i] : p.ulen) : 0u;
+        OctBlock B;
+        oct_block<kVerify>(p, B, off, L, valid, lo, b, lane);
+        const bool need = valid && !((B.mine >> lane) & 1ull);
+        if (__ballot(need) == 0ull) continue;
+        if (need) {
+            const uint8_t *pkt = p.base + off;
+            const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | L) & 3u) == 0;
+            uint32_t h[18];
+#pragma unroll
+            for (uint32_t k = 0; k < 18; ++k) {
+                uint32_t x = 0;
+                if (k >= 7u && L >= ICRC_MIN_PACKET && 4u * k + 8u <= L + (fast ? 0u : 3u)) {
+                    if (fast) {
+                        x = *reinterpret_cast<const uint32_t *>(pkt + 4u * k);
+                    } else {
+#pragma unroll
+                        for (uint32_t t = 0; t < 4; ++t) {
+                            const uint32_t o = 4u * k + t;
+                            x |= (o + 4u < L ? static_cast<uint32_t>(pkt[o]) : 0u) << (8u * t);
+                        }
+                    }
+                }
+                h[k] = x;
+            }
+            uint32_t v[18];
+            rx_decode(h, off, L, p.ok[i], v);
+            uint32_t *d = reinterpret_cast<uint32_t *>(p.rx + i);
+#pragma unroll
+            for (uint32_t k = 0; k < 18; ++k) d[k] = v[k];
+        }
+    }
+}
+
+template <bool TRAILER>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_rx_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    uint32_t lo, nq;
+    bool rest = false;  // this wave's range has packets the ring left (the sweep's)
+    const bool any = rx_oct_part<TRAILER, OctProduct, true>(p, lds4, lo, nq, &rest);
+    __syncthreads();  // every wave is done with the receive image before the long body rewrites LDS
+    long_body<kVerify, false, TRAILER>(p, lds4, blockIdx.x, gridDim.x);
+    __syncthreads();  // the long packets' ok bytes are in p.ok
+    if (any && rest) rx_sweep(p, lo, nq, threadIdx.x & 63u);
 }
 
 #ifdef ICRC_AB_BUILD
@@ -1097,6 +1223,13 @@ int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag) {
 #endif
     if (p.trailer) hipLaunchKernelGGL((icrc_oct_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     else hipLaunchKernelGGL((icrc_oct_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
+}
+
+int launch_hybrid_rx(const BatchParams &p, int grid, void *stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    else hipLaunchKernelGGL((icrc_hybrid_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

@@ -914,6 +914,58 @@ def test_rx_parse_strided_short_one_pass_full_blocks(engine, L):
     np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
 
 
+@pytest.mark.parametrize("zero_trailer", [False, True])
+def test_rx_parse_ragged_one_pass(engine, zero_trailer):
+    """Ragged batches with more than 32 packets per wave take ONE launch (icrc_hybrid_rx_kernel):
+    the one-pass receive on the oct kernel's packets, then long_body's verify and a sweep for the
+    rest.  Mostly 316-B packets with 1084 / 1088 / 1089 / 4156 / 2001-B ones, short (44, 48, 60)
+    and odd-length (61) ones, 3 % starting off a word boundary, one flipped ICRC per 29 packets;
+    descriptors, ok bytes and trailers against the oracle, and the descriptors with no ok array."""
+    import icrc_amd
+    import rx_cases
+
+    rng = np.random.default_rng(31 + int(zero_trailer))
+    n = torch.cuda.get_device_properties(0).multi_processor_count * 16 * 32 + 5003
+    corpus = [p for p in rx_cases.make_packets(rng) if p.size >= 44]
+    lens = rng.choice([316, 1084, 1088, 1089, 4156, 2001, 44, 48, 60, 61], n,
+                      p=[0.80, 0.05, 0.02, 0.02, 0.05, 0.02, 0.01, 0.01, 0.01, 0.01]).astype(np.uint32)
+    gaps = rng.integers(1, 4, n) * (rng.random(n) < 0.03)
+    off = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        off[i] = pos
+        pos += int(lens[i])
+    buf = rng.integers(0, 256, pos + 8, dtype=np.uint8)
+    for i in range(n):
+        t = corpus[i % len(corpus)]
+        m = min(int(lens[i]) - 4, t.size - 4)
+        buf[int(off[i]): int(off[i]) + m] = t[:m]
+    ic = oracle.compute_icrc_batch(buf, off, lens)
+    tr = (off + lens - 4).astype(np.int64)
+    for k in range(4):
+        buf[tr + k] = ((ic >> (8 * k)) & 0xFF).astype(np.uint8)
+    buf[tr[::29]] ^= 0x40
+    ref = buf.copy()
+    want = oracle.rx_parse(ref, off, lens, zero_trailer=zero_trailer)
+    for with_ok in (True, False):
+        d_buf = dev(buf)
+        d_off, d_len = dev(off), dev(lens)
+        d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+        d_ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        d_nerr = torch.zeros(1, dtype=torch.int32, device="cuda")
+        engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(),
+                        d_ok.data_ptr() if with_ok else 0, zero_trailer=zero_trailer, d_nerr=d_nerr.data_ptr(),
+                        stream=stream_handle())
+        torch.cuda.synchronize()
+        got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+        assert_desc_equal(got, want)
+        if with_ok:
+            np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
+        np.testing.assert_array_equal(d_buf.cpu().numpy(), ref)
+    assert int(np.sum(want["status"] == 0)) > n // 2 and int(np.sum(want["icrc_ok"] == 0)) >= n // 29
+
+
 def test_send_receive_roundtrip(engine):
     """Packetize 24 WRITE / READ RESPONSE messages on the GPU, parse them on the GPU, and place each
     payload at its RETH va: the memory region equals the source bytes (C3 closed on-device)."""
