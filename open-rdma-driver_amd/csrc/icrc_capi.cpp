@@ -1399,10 +1399,10 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
         p.table_oct = e->d_table_oct;
         return icrc::launch_oct_rx(p, grid_for(e, n), stream, rx_oct_knob());
     }
-    // Ragged batches with whole 64-packet blocks per wave: ONE launch (icrc_hybrid_rx_kernel): the
-    // same one-pass receive on the packets the oct kernel takes, the long-packet verify on the rest,
-    // then their descriptors from their header words.  p.ok carries the long packets' results to
-    // that last step: a stream-ordered scratch array when the caller passes none.  (A/B:
+    // Ragged batches with whole 64-packet blocks per wave: the same one-pass receive on the packets
+    // the oct kernel takes and the long-packet verify on the rest in one launch, then descriptors
+    // for the rest from their header words (icrc_rx_sweep_kernel).  p.ok carries the long packets'
+    // results to that last step: a stream-ordered scratch array when the caller passes none.  (A/B:
     // ICRC_AB_RX_OCT=0 keeps the two passes.)
     {
         const int grid = grid_for(e, n);
@@ -1414,7 +1414,7 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
             hipStream_t s = static_cast<hipStream_t>(stream);
             if (!d_ok) HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&scratch), n, s));
             p.ok = d_ok ? d_ok : scratch;
-            int rc = icrc::launch_hybrid_rx(p, grid, stream);
+            int rc = icrc::launch_hybrid_rx(p, grid, e->num_cu, stream);
             if (scratch && hipFreeAsync(scratch, s) != hipSuccess && rc == ICRC_OK) rc = ICRC_EDEVICE;
             return rc;
         }

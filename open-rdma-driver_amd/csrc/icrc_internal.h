@@ -124,10 +124,11 @@ uint32_t oct_max_len();
 // strided batch whose packets are all the oct kernel's (44 <= L <= oct_max_len(), 4-aligned).
 // diag (A/B library only, ICRC_AB_RX_OCT=2..5): the kernel's cuts (OctRxAblation, icrc_oct.hip).
 int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag = 0);
-// The same for ragged batches (icrc_hybrid_rx_kernel): the oct ring on L < p.split_len, long_body's
-// verify on the rest, then descriptors for every packet the ring did not take; p.ok must be set.
-// Workgroup ranges must be whole 64-packet blocks (more than 32 packets per wave of the grid).
-int launch_hybrid_rx(const BatchParams &p, int grid, void *stream);
+// The same for ragged batches, two launches (icrc_hybrid_rx_kernel: the oct ring on L < p.split_len,
+// long_body's verify on the rest; icrc_rx_sweep_kernel: descriptors for every packet the ring did not
+// take); p.ok must be set.  Workgroup ranges must be whole 64-packet blocks (more than 32 packets
+// per wave of the grid).
+int launch_hybrid_rx(const BatchParams &p, int grid, int num_cu, void *stream);
 // The hybrid dispatch with the oct kernel as its short-packet half, in one launch (icrc_oct.hip):
 // grid_oct workgroups of the oct kernel, then grid_long of the long-packet kernel.
 int launch_hybrid(int mode, const BatchParams &p, int grid_oct, int grid_long, void *stream);

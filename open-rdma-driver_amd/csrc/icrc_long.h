@@ -360,6 +360,93 @@ __device__ __forceinline__ void rx_decode(const uint32_t (&h)[18], uint64_t off,
     v[17] = (okb & 0xFFu) | (status << 8);
 }
 
+// ---- the descriptor pass's block (icrc_rx_desc_kernel, icrc_kernels.hip; the one-pass ragged
+// receive's sweep, icrc_oct.hip) --------------------------------------------------------------
+// Packets base .. base + cnt - 1 whose bit is set in keep get their descriptors (the others are
+// neither read nor written).  Header words are loaded three packets per instruction (11 lanes
+// each, words 7..17 -- bytes 28..71: rx_decode reads nothing of the IPv4 / UDP header, so those
+// lines are not fetched), transposed through LDS (sh: 64 x kRxStride words of this wave) to lane =
+// packet for the decode, and transposed back so the descriptors leave as 18 coalesced dword stores.
+constexpr uint32_t kRxStride = 19;  // LDS words per packet row (odd: conflict-free lane = packet reads)
+constexpr uint32_t kRxWord0 = 7, kRxHdrWords = 11;             // header words the decode reads: 7..17
+constexpr uint32_t kRxGroups = 64u / kRxHdrWords;              // packets per load round (5)
+constexpr uint32_t kRxRounds = (64u + kRxGroups - 1u) / kRxGroups;  // 13
+__device__ __forceinline__ void rx_desc_block(const BatchParams &p, uint32_t *sh, uint32_t base, uint32_t cnt, uint64_t keep,
+                                              uint32_t lane) {
+    const uint32_t g = lane / kRxHdrWords, w = kRxWord0 + lane - kRxHdrWords * g;
+    {
+        const uint32_t i = base + lane;
+        const bool in = lane < cnt && ((keep >> lane) & 1ull);
+        const uint64_t off = in ? (p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride) : 0u;
+        const uint32_t L = in ? (p.len ? p.len[i] : p.ulen) : 0u;
+        const uint32_t okb = in ? p.ok[i] : 0u;  // from the verify pass
+        const uint8_t *pkt = p.base + off;
+        const bool fast = L >= ICRC_MIN_PACKET && ((reinterpret_cast<uintptr_t>(pkt) | static_cast<uintptr_t>(L)) & 3u) == 0;
+        const uint32_t olo = static_cast<uint32_t>(off), ohi = static_cast<uint32_t>(off >> 32);
+        const uint32_t lf = fast ? L : 0u;  // 0: not loaded here (short / irregular)
+        // All 22 rounds of header loads go out before any is used (a load under a branch made every
+        // round wait for the one before: 60-76 us per 786 K packets), so every lane loads: one with
+        // nothing to load reads the first word of the group's first fast packet and drops it.
+        const uint64_t fm = __builtin_amdgcn_ballot_w64(fast);
+        if (fm != 0u) {
+            const int f0 = __builtin_ctzll(fm);
+            const uint32_t dlo = static_cast<uint32_t>(__builtin_amdgcn_readlane(olo, f0));  // int: no sign extension
+            const uint32_t dhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(ohi, f0));
+            const uint8_t *dq = p.base + (static_cast<uint64_t>(dlo) | (static_cast<uint64_t>(dhi) << 32));
+            uint32_t hv[kRxRounds];
+#pragma unroll
+            for (uint32_t r = 0; r < kRxRounds; ++r) {  // kRxGroups packets per round
+                const uint32_t j = kRxGroups * r + g;
+                const int src = static_cast<int>((j & 63u) << 2);
+                const uint32_t jl = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lf)));
+                const uint32_t jlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(olo)));
+                const uint32_t jhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ohi)));
+                const bool k = g < kRxGroups && j < 64u && 4u * w + 8u <= jl;  // jl = 0 for packets not on this path
+                const uint8_t *q =
+                    k ? p.base + (static_cast<uint64_t>(jlo) | (static_cast<uint64_t>(jhi) << 32)) + 4u * w : dq;
+                hv[r] = *reinterpret_cast<const uint32_t *>(q);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < kRxRounds; ++r) {
+                const uint32_t j = kRxGroups * r + g;
+                if (g < kRxGroups && j < 64u) sh[j * kRxStride + w] = hv[r];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t h[18];
+#pragma unroll
+        for (uint32_t k = 0; k < 18; ++k) {  // words not loaded (dummy reads, short packets, 0..6) read as 0
+            const uint32_t x = k >= kRxWord0 ? sh[lane * kRxStride + k] : 0u;
+            h[k] = (fast && 4u * k + 8u <= L) ? x : 0u;
+        }
+        if (!fast && L >= ICRC_MIN_PACKET) {  // misaligned or L % 4 != 0: byte-wise, this lane only
+#pragma unroll
+            for (uint32_t k = kRxWord0; k < 18; ++k) {
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const uint32_t o = 4u * k + t;
+                    x |= (o + 4u < L ? static_cast<uint32_t>(pkt[o]) : 0u) << (8u * t);
+                }
+                h[k] = x;
+            }
+        }
+        uint32_t v[18];
+        rx_decode(h, off, L, okb, v);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t k = 0; k < 18; ++k) sh[lane * kRxStride + k] = v[k];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t *dst = reinterpret_cast<uint32_t *>(p.rx + base);
+#pragma unroll
+        for (uint32_t t = 0; t < 18; ++t) {
+            const uint32_t idx = t * 64u + lane, pk = idx / 18u, k = idx - 18u * pk;
+            if (pk < cnt && ((keep >> pk) & 1ull)) dst[idx] = sh[pk * kRxStride + k];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // PARSE = 2, the fused receive parse of the one-packet pipeline (small batches, icrc_rx_kernel):
 // no store per packet (a store in the ring makes hipcc wait for zero there, draining the prefetch).  Each packet's header words
 // (lane w = word w, from its rows as loaded), offset and length go into lane q & 63 of these

@@ -414,7 +414,7 @@ __device__ __forceinline__ uint32_t rx_ent(uint32_t i, uint32_t k) {
 
 template <int MODE, bool RAGGED, bool TRAILER, class D, bool RX = false>
 __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, const LaneConsts &c, uint32_t lane,
-                                        uint32_t lo, uint32_t nq, bool *rx_rest = nullptr) {
+                                        uint32_t lo, uint32_t nq) {
     constexpr bool kPrio = kOctPrio && D::kPrio;
     constexpr int K = kOctK;
     constexpr int P = kOctPairs;  // ring positions, two frames (slots 2 p, 2 p + 1) each
@@ -874,10 +874,6 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
             } else if (oct_block<MODE>(p, NB, off, L, valid, lo, nb_next, lane) != 0) {
                 irregular = true;
             }
-            if constexpr (RX && RAGGED) {
-                // packets left for the sweep (not this ring's: long, irregular)?
-                if (rx_rest && (__ballot(valid) & ~NB.mine) != 0ull) *rx_rest = true;
-            }
             if constexpr (RX && RAGGED) {  // the block's base offset into the record's ring (row 18, entries 32..47)
                 const uint32_t e = rx_wb + rx_ent(32u + 2u * (static_cast<uint32_t>(nb_next) & 7u) + (lane & 1u), kRxDummyRow);
                 const uint32_t v = (lane & 1u) ? static_cast<uint32_t>(NB.boff >> 32) : static_cast<uint32_t>(NB.boff);
@@ -1016,8 +1012,24 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_self_kernel(Batc
 // The oct half of a receive kernel on workgroup blockIdx.x: the receive image, then run_oct (RX) on
 // this wave's range [lo, lo + nq); false if the wave has no range.
 template <bool TRAILER, class D, bool RAGGED>
-__device__ __forceinline__ bool rx_oct_part(const BatchParams &p, uint4 *lds4, uint32_t &lo, uint32_t &nq,
-                                            bool *rest = nullptr) {
+__device__ __forceinline__ bool rx_oct_part(const BatchParams &p, uint4 *lds4, uint32_t &lo, uint32_t &nq) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t tw = gridDim.x * kWavesPerGroup;
+    uint32_t chunk = (p.n + tw - 1) / tw;
+    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 7u) & ~7u;
+    uint64_t lo64, hi64;
+    wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew & 0xFFFFu, lo64, hi64);
+    const bool mine = lo64 < p.n;
+    lo = mine ? static_cast<uint32_t>(lo64) : 0u;
+    nq = mine ? static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64) : 0u;
+    if (RAGGED && p.split_len != 0 && p.len != nullptr) {
+        // A workgroup whose packets are all long skips the ring (and its table image): the sweep
+        // takes every packet.
+        const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk;
+        const uint64_t g1 = g0 + static_cast<uint64_t>(kWavesPerGroup) * chunk;
+        if (!wg_any_split<true>(p, lds4, g0, g1 < p.n ? g1 : p.n)) return mine;
+    }
     {   // thread t: bulk entry t's 16 copies (lower half of its table row) and 16 bytes of the final
         // tables (row t >> 3, lanes 4 (t & 7) .. + 3 of the compact form's 64-lane rows)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1034,20 +1046,11 @@ __device__ __forceinline__ bool rx_oct_part(const BatchParams &p, uint4 *lds4, u
         __syncthreads();
     }
     const char *lds = reinterpret_cast<const char *>(lds4);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     LaneConsts c;
     c.pc = ((lane & 15u) * 4u) | (((lane & 15u) * 4u + 64u) << 8) | (1u << 16);
     c.fin = 128u + (lane & 31u) * 4u;
-    const uint32_t tw = gridDim.x * kWavesPerGroup;
-    uint32_t chunk = (p.n + tw - 1) / tw;
-    chunk = chunk > 32u ? (chunk + 63u) & ~63u : (chunk + 7u) & ~7u;
-    uint64_t lo64, hi64;
-    wave_range(static_cast<uint64_t>(blockIdx.x) * kWavesPerGroup * chunk, chunk, wave, p.skew & 0xFFFFu, lo64, hi64);
-    if (lo64 >= p.n) return false;
-    lo = static_cast<uint32_t>(lo64);
-    nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
-    run_oct<kVerify, RAGGED, TRAILER, D, true>(p, lds, c, lane, lo, nq, rest);
+    if (!mine) return false;
+    run_oct<kVerify, RAGGED, TRAILER, D, true>(p, lds, c, lane, lo, nq);
     return true;
 }
 
@@ -1058,64 +1061,40 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_oct_rx_kernel(BatchPara
     rx_oct_part<TRAILER, D, false>(p, lds4, lo, nq);
 }
 
-// The ragged one-pass receive: the packets the oct ring decoded keep their descriptors; the rest of
-// the wave's range (L >= split_len: verified by long_body; L < 44, misaligned, far apart: the oct
-// tail loop) are decoded here, lane = packet, from their header words and the ok bytes those paths
-// left in p.ok (a workgroup barrier before this: the long-packet waves are other waves of the same
-// workgroup, on the same workgroup range).  Their descriptors are stored lane = packet, outside any
-// load ring.
-__device__ __forceinline__ void rx_sweep(const BatchParams &p, uint32_t lo, uint32_t nq, uint32_t lane) {
-    __builtin_amdgcn_s_waitcnt(0);  // the ring's descriptor stores (garbage for these packets) land first
-    const int nblocks = static_cast<int>((nq + 63u) >> 6);
-    for (int b = 0; b < nblocks; ++b) {
-        const uint32_t q = static_cast<uint32_t>(b) * 64u + lane;
-        const bool valid = q < nq;
-        const uint32_t i = lo + q;
-        const uint64_t off = valid ? (p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride) : 0u;
-        const uint32_t L = valid ? (p.len ? p.len[i] : p.ulen) : 0u;
-        OctBlock B;
-        oct_block<kVerify>(p, B, off, L, valid, lo, b, lane);
-        const bool need = valid && !((B.mine >> lane) & 1ull);
-        if (__ballot(need) == 0ull) continue;
-        if (need) {
-            const uint8_t *pkt = p.base + off;
-            const bool fast = ((reinterpret_cast<uintptr_t>(pkt) | L) & 3u) == 0;
-            uint32_t h[18];
-#pragma unroll
-            for (uint32_t k = 0; k < 18; ++k) {
-                uint32_t x = 0;
-                if (k >= 7u && L >= ICRC_MIN_PACKET && 4u * k + 8u <= L + (fast ? 0u : 3u)) {
-                    if (fast) {
-                        x = *reinterpret_cast<const uint32_t *>(pkt + 4u * k);
-                    } else {
-#pragma unroll
-                        for (uint32_t t = 0; t < 4; ++t) {
-                            const uint32_t o = 4u * k + t;
-                            x |= (o + 4u < L ? static_cast<uint32_t>(pkt[o]) : 0u) << (8u * t);
-                        }
-                    }
-                }
-                h[k] = x;
-            }
-            uint32_t v[18];
-            rx_decode(h, off, L, p.ok[i], v);
-            uint32_t *d = reinterpret_cast<uint32_t *>(p.rx + i);
-#pragma unroll
-            for (uint32_t k = 0; k < 18; ++k) d[k] = v[k];
-        }
-    }
-}
-
+// The ragged one-pass receive, launch 1 of 2: the oct ring (RX) on the workgroup's packets with L <
+// split_len (a workgroup with none skips it), then long_body's verify of the rest.
 template <bool TRAILER>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_rx_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
     uint32_t lo, nq;
-    bool rest = false;  // this wave's range has packets the ring left (the sweep's)
-    const bool any = rx_oct_part<TRAILER, OctProduct, true>(p, lds4, lo, nq, &rest);
+    rx_oct_part<TRAILER, OctProduct, true>(p, lds4, lo, nq);
     __syncthreads();  // every wave is done with the receive image before the long body rewrites LDS
     long_body<kVerify, false, TRAILER>(p, lds4, blockIdx.x, gridDim.x);
-    __syncthreads();  // the long packets' ok bytes are in p.ok
-    if (any && rest) rx_sweep(p, lo, nq, threadIdx.x & 63u);
+}
+
+// Launch 2: descriptors for every packet the ring did not take (L >= split_len, verified by
+// long_body; L < 44, misaligned, far apart: the ring's tail loop), from their header words and the
+// ok bytes those paths left in p.ok, in the descriptor pass's shape (rx_desc_block).  The ring's
+// blocks are whole, 64-aligned blocks of the batch (the dispatch guarantees more than 32 packets
+// per wave), so classifying each block here again (oct_block) finds exactly the ring's packets.
+// (In the first launch, after long_body, this measured slower: that kernel's registers are sized
+// for its rings.)
+__global__ __launch_bounds__(256) void icrc_rx_sweep_kernel(BatchParams p) {
+    __shared__ uint32_t sh_all[4 * 64 * kRxStride];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *sh = sh_all + wave * 64u * kRxStride;
+    const uint32_t tw = gridDim.x * 4u;
+    for (uint32_t base = (blockIdx.x * 4u + wave) * 64u; base < p.n; base += tw * 64u) {
+        const uint32_t i = base + lane;
+        const bool valid = i < p.n;
+        const uint64_t off = valid ? (p.off ? p.off[i] : static_cast<uint64_t>(i) * p.stride) : 0u;
+        const uint32_t L = valid ? (p.len ? p.len[i] : p.ulen) : 0u;
+        OctBlock B;
+        oct_block<kVerify>(p, B, off, L, valid, base, 0, lane);
+        const uint64_t need = __ballot(valid) & ~B.mine;
+        if (need != 0ull) rx_desc_block(p, sh, base, p.n - base < 64u ? p.n - base : 64u, need, lane);
+    }
 }
 
 #ifdef ICRC_AB_BUILD
@@ -1226,10 +1205,14 @@ int launch_oct_rx(const BatchParams &p, int grid, void *stream, int diag) {
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 
-int launch_hybrid_rx(const BatchParams &p, int grid, void *stream) {
+int launch_hybrid_rx(const BatchParams &p, int grid, int num_cu, void *stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     else hipLaunchKernelGGL((icrc_hybrid_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
+    if (hipGetLastError() != hipSuccess) return ICRC_EDEVICE;
+    const uint64_t want = (static_cast<uint64_t>(p.n) + 255u) / 256u;
+    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u;
+    hipLaunchKernelGGL(icrc_rx_sweep_kernel, dim3(static_cast<uint32_t>(want < cap ? want : cap)), dim3(256), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
 

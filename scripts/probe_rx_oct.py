@@ -28,7 +28,8 @@ def main():
               ("1Mi x 1084 B", workloads.write_middle_stream(1 << 20, pmtu=1024), False)]
     if os.environ.get("RAGGED"):  # the same through (offset, length) arrays, and configs[2]
         shapes = [("4Mi x 316 B ragged", workloads.write_middle_stream(4 << 20, pmtu=256), True),
-                  ("C2 mixed MTU", workloads.mixed_mtu_stream(4 << 20), True)]
+                  ("C2 mixed MTU", workloads.mixed_mtu_stream(4 << 20), True),
+                  ("786K x 4156 B ragged", workloads.write_middle_stream(786432), True)]
     for name, w, ragged in shapes:
         L = int(w.lens[0])
         b = workloads.synthesize(eng, w, stream=s)
