@@ -236,6 +236,11 @@ def main(argv=None) -> int:
     if world != args.gpus:
         log(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
         return 2
+    if os.environ.get("BENCH_DUMP_MAPS"):  # diagnostics: the address map at the end of the Python exit path
+        import atexit
+        import shutil
+
+        atexit.register(shutil.copyfile, "/proc/self/maps", os.environ["BENCH_DUMP_MAPS"])
     if args.cpu_stub:
         return run_cpu_stub(args, rank, world)
     return run_gpu(args, rank, world, local)
@@ -272,7 +277,7 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
     if args.only == "rx":
         rx = receive_short(eng, stream, args, world)
         print(json.dumps(rx), flush=True)
-        return 0 if all(v["all_ok"] for v in rx.values()) else 1
+        return 0 if all(v["all_ok"] and not v.get("parity_failures") for v in rx.values()) else 1
     if args.only == "msg":
         msg = host_message_c0(eng, stream, args)
         print(json.dumps(msg), flush=True)
@@ -386,8 +391,14 @@ def run_gpu(args, rank: int, world: int, local: int) -> int:
         torch.cuda.empty_cache()
         c2, f2 = config_c2(eng, stream, args, world, orc)
         c3, f3 = config_c3(eng, stream, args, world, orc)
-        result["configs"] = {"c2": c2, "c3": c3}
-        cfg_fails = f2 + f3
+        c2rx, f2rx = config_c2_rx(eng, stream, args, world, orc)
+        result["configs"] = {"c2": c2, "c3": c3, "c2_rx": c2rx}
+        cfg_fails += f2rx
+        c0 = config_c0_native()
+        if c0 is not None:
+            result["configs"]["c0_msg"] = c0
+            cfg_fails += 0 if c0.get("bad", 1) == 0 else 1
+        cfg_fails += f2 + f3
 
     if args.extra:
         result["extra"] = extra_measurements(eng, stream, args, world)
@@ -472,10 +483,47 @@ def config_c3(eng, stream, args, world, orc):
     leg = {"workload": "configs[3]: 16 MiB RDMA WRITE at PMTU 4096 (4096 packets), compute + write_trailer then "
                        "verify + zero_trailer",
            "packets": w3.n, "ms_per_roundtrip": round(kms, 4),
-           "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1), "all_ok": all_ok,
-           "parity_checked": w3.n, "parity_failures": fails}
+           "GiB/s_per_direction": round(2 * tot3 / (kms * 1e-3) / GIB, 1),
+           "frac": round(2 * tot3 / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_note": "per direction: packet bytes / (round trip / 2) / 8 TB/s (HIP events over back-to-back "
+                        "launches: the two kernels and the gaps between them)",
+           "all_ok": all_ok, "parity_checked": w3.n, "parity_failures": fails}
     del d_buf, d_off, d_len, d_out, d_ok
     return leg, fails + (0 if all_ok else 1)
+
+
+def config_c0_native():
+    """configs[0] in the default line: one QP's 64 x 4156-B RDMA WRITE per
+    message, compute + write_trailer then verify + zero_trailer, from 1 and 3 NATIVE threads (the
+    emulator's send, packet-handler and receive threads are Rust, not Python: scripts/_build/msg_probe,
+    C++) through the submission ring, pinned message buffers, ~0.5 s.  None when the probe is not
+    built."""
+    import icrc_amd
+
+    probe = os.path.join(ROOT, "scripts", "_build", "msg_probe")
+    if not os.path.exists(probe):
+        return None
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(icrc_amd.LIB_PATH), MSG_PROBE_PATH="ring",
+               MSG_PROBE_KINDS="pinned")
+    try:
+        r = subprocess.run([probe, "6000", "1", "3"], capture_output=True, text=True, timeout=60, env=env)
+        rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    except (subprocess.TimeoutExpired, ValueError) as e:
+        return {"error": f"msg_probe: {e}"}
+    runs = [x for x in rows if "threads" in x]
+    stats = next((x for x in rows if "ring_jobs" in x), {})
+    if r.returncode != 0 or len(runs) != 2:
+        return {"error": f"msg_probe exit {r.returncode}", "stderr": r.stderr[-400:]}
+    one, three = runs
+    return {"workload": "configs[0]: 64 x 4156-B RDMA WRITE per message in pinned host memory, compute + "
+                        "write_trailer then verify + zero_trailer, native threads through the submission ring",
+            "messages_per_s_1_thread": one["messages_per_s"], "p50_us_1_thread": one["message_p50_us"],
+            "p99_us_1_thread": one["message_p99_us"],
+            "messages_per_s_3_threads": three["messages_per_s"], "p50_us_3_threads": three["message_p50_us"],
+            "p99_us_3_threads": three["message_p99_us"],
+            "GiB/s_3_threads": round(three["messages_per_s"] * 64 * 4156 / GIB, 2),
+            "calls_per_thread": 6000, "bad": one["bad"] + three["bad"],
+            "ring": {k: stats.get(k) for k in ("ring_jobs", "ring_launches", "ring_relaunches", "ring_timeouts")}}
 
 
 def per_rank_fields(rows):
@@ -816,50 +864,89 @@ def fused_send_receive(eng, stream, args, world):
     return out
 
 
-def receive_short(eng, stream, args, world):
-    """§8f row 3 at the emulator's receive shapes: icrc_rx_parse_device (verify + strip + parse)
-    over configs[2]'s mixed-MTU batch with its trailers written (`rx_verify_parse_c2`), and over 4 Mi
-    316-byte packets (the 256-B MTU class) as a ragged batch and as a strided one.  Algorithmic HBM
-    bytes per packet: the packet read + a 72-byte descriptor + an ok byte written."""
+def rx_leg(eng, stream, args, world, w, ragged, orc=None, sample=0):
+    """One receive leg: w's packets synthesised, their trailers written by a compute pass, then
+    icrc_rx_parse_device (verify + strip + parse) timed like the headline.  sample > 0: the first and
+    last `sample` packets' descriptors and ok bytes against the oracle's rx_parse (the checker)."""
     import torch
 
     import icrc_amd
     from icrc_amd import workloads
 
-    out = {}
     desc_b = icrc_amd.RX_DESC_DTYPE.itemsize
+    d_buf = workloads.synthesize(eng, w, stream=stream)
+    d_off, d_len = dev(w.off), dev(w.lens)
+    d_tmp = torch.zeros(w.n, dtype=torch.int32, device="cuda")
+    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_tmp.data_ptr(), True, 0, stream)
+    torch.cuda.synchronize()
+    del d_tmp
+    d_desc = torch.empty(w.n * desc_b, dtype=torch.uint8, device="cuda")
+    d_ok = torch.zeros(w.n, dtype=torch.uint8, device="cuda")
+    L = int(w.lens[0])
+    if ragged:
+        fn = lambda: eng.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_desc.data_ptr(),
+                                  d_ok.data_ptr(), stream=stream)
+    else:
+        fn = lambda: eng.rx_parse(d_buf.data_ptr(), 0, 0, w.n, d_desc.data_ptr(), d_ok.data_ptr(),
+                                  stride=L, length=L, stream=stream)
+    _, kms = time_kernel(fn, min(args.steps, 20), min(args.warmup, 5), world)
+    tot = int(w.lens.astype(np.uint64).sum())
+    alg = tot + w.n * (desc_b + 1)
+    desc = d_desc[: 64 * desc_b].cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+    res = {"packets": w.n, "packet_bytes": tot, "kernel_ms": round(kms, 4),
+           "hbm_GB/s": round(alg / (kms * 1e-3) / 1e9, 1), "frac_of_peak": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "all_ok": bool((d_ok == 1).all().item()), "first_desc_payload_len": int(desc["payload_len"][0])}
+    if sample and orc is not None:
+        got_all = d_desc.view(w.n, desc_b)
+        fails = 0
+        for a, b in ((0, min(sample, w.n)), (max(0, w.n - sample), w.n)):
+            lo, hi = int(w.off[a]), int(w.off[b - 1]) + int(w.lens[b - 1])
+            host = d_buf[lo:hi].cpu().numpy()
+            want = orc.rx_parse(host, (w.off[a:b] - np.uint64(lo)).astype(np.uint64), w.lens[a:b])
+            got = got_all[a:b].cpu().numpy().reshape(-1).view(icrc_amd.RX_DESC_DTYPE).copy()
+            # the oracle parsed the sample from offset 0 (payload_offset is 0 on a packet that failed to parse)
+            got["payload_offset"] = np.where(got["status"] == 0, got["payload_offset"] - np.uint64(lo),
+                                             got["payload_offset"])
+            for f in want.dtype.names:
+                if f != "_pad":
+                    fails += int(np.count_nonzero(got[f] != want[f]))
+            fails += int(np.count_nonzero(d_ok[a:b].cpu().numpy() != want["icrc_ok"]))
+        res["parity_checked"] = 2 * min(sample, w.n)
+        res["parity_failures"] = fails
+    del d_buf, d_off, d_len, d_desc, d_ok
+    torch.cuda.empty_cache()
+    return res
 
-    def leg(w, ragged):
-        d_buf = workloads.synthesize(eng, w, stream=stream)
-        d_off, d_len = dev(w.off), dev(w.lens)
-        d_tmp = torch.zeros(w.n, dtype=torch.int32, device="cuda")
-        eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_tmp.data_ptr(), True, 0, stream)
-        torch.cuda.synchronize()
-        del d_tmp
-        d_desc = torch.empty(w.n * desc_b, dtype=torch.uint8, device="cuda")
-        d_ok = torch.zeros(w.n, dtype=torch.uint8, device="cuda")
-        L = int(w.lens[0])
-        if ragged:
-            fn = lambda: eng.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w.n, d_desc.data_ptr(),
-                                      d_ok.data_ptr(), stream=stream)
-        else:
-            fn = lambda: eng.rx_parse(d_buf.data_ptr(), 0, 0, w.n, d_desc.data_ptr(), d_ok.data_ptr(),
-                                      stride=L, length=L, stream=stream)
-        _, kms = time_kernel(fn, min(args.steps, 20), min(args.warmup, 5), world)
-        tot = int(w.lens.astype(np.uint64).sum())
-        alg = tot + w.n * (desc_b + 1)
-        desc = d_desc[: 64 * desc_b].cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
-        res = {"packets": w.n, "packet_bytes": tot, "kernel_ms": round(kms, 4),
-               "hbm_GB/s": round(alg / (kms * 1e-3) / 1e9, 1), "frac_of_peak": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-               "all_ok": bool((d_ok == 1).all().item()), "first_desc_payload_len": int(desc["payload_len"][0])}
-        del d_buf, d_off, d_len, d_desc, d_ok
-        torch.cuda.empty_cache()
-        return res
 
-    out["rx_verify_parse_c2"] = leg(workloads.mixed_mtu_stream(4 << 20), True)
+def config_c2_rx(eng, stream, args, world, orc):
+    """configs[2]'s batch through the receive parse: mixed_mtu_stream(4 Mi) with
+    its trailers written, icrc_rx_parse_device on the default ragged dispatch; algorithmic bytes =
+    packets read + a 72-byte descriptor and an ok byte written per packet; 4096 descriptors (both ends)
+    against the oracle.  Returns (leg, mismatches)."""
+    from icrc_amd import workloads
+
+    r = rx_leg(eng, stream, args, world, workloads.mixed_mtu_stream(4 << 20), True, orc, 2048)
+    leg = {"workload": "configs[2] received: 4 Mi mixed-MTU packets, icrc_rx_parse_device (verify + strip + parse "
+                       "into 72-byte descriptors), ragged arrays",
+           "packets": r["packets"], "kernel_ms": r["kernel_ms"], "hbm_GB/s": r["hbm_GB/s"], "frac": r["frac_of_peak"],
+           "all_ok": r["all_ok"], "parity_checked": r["parity_checked"], "parity_failures": r["parity_failures"]}
+    return leg, r["parity_failures"] + (0 if r["all_ok"] else 1)
+
+
+def receive_short(eng, stream, args, world):
+    """§8f row 3 at the emulator's receive shapes: icrc_rx_parse_device (verify + strip + parse)
+    over configs[2]'s mixed-MTU batch with its trailers written (`rx_verify_parse_c2`, with 4096
+    descriptors checked against the oracle), and over 4 Mi 316-byte packets (the 256-B MTU class) as
+    a ragged batch and as a strided one.  Algorithmic HBM bytes per packet: the packet read + a
+    72-byte descriptor + an ok byte written."""
+    import oracle as orc
+    from icrc_amd import workloads
+
+    out = {}
+    out["rx_verify_parse_c2"] = rx_leg(eng, stream, args, world, workloads.mixed_mtu_stream(4 << 20), True, orc, 2048)
     w316 = workloads.write_middle_stream(4 << 20, 256)
-    out["rx_verify_parse_316_ragged"] = leg(w316, True)
-    out["rx_verify_parse_316_strided"] = leg(w316, False)
+    out["rx_verify_parse_316_ragged"] = rx_leg(eng, stream, args, world, w316, True, orc, 2048)
+    out["rx_verify_parse_316_strided"] = rx_leg(eng, stream, args, world, w316, False, orc, 2048)
     return out
 
 

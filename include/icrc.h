@@ -35,8 +35,9 @@
  *     submission ring: a resident service kernel polls the ring's slots in pinned host memory (the
  *     emulator's doorbell / descriptor-queue model, queues/send/queue.rs:66-100), so a call costs
  *     no kernel launch; the kernel (eight 256-thread workgroups per slot: 32 CUs) ends between jobs after 1 ms
- *     of life or 2 ms without calls and the next call starts it again, and a job not done within
- *     2 s fails with ICRC_ETIMEDOUT.  Up to four messages run at once (the emulator's three
+ *     of life or 2 ms without calls and the next call starts it again; a job not done within 2 s
+ *     retires the ring (counted in icrc_engine_host_stats out[3]) and the call, and every later
+ *     one, runs as a kernel launch instead.  Up to four messages run at once (the emulator's three
  *     threads each get one); more callers wait for a slot.  ICRC_HOST_LAUNCH
  *     (icrc_engine_set_host_path) runs each message as a kernel launch instead, through a
  *     four-stream submitter that merges callers beyond four into one launch.  Larger host batches
@@ -60,7 +61,7 @@ extern "C" {
 #define ICRC_ENOMEM (-12)  /* host or device allocation failed                           */
 #define ICRC_ENODEV (-19)  /* no usable GPU / engine for the requested device             */
 #define ICRC_EDEVICE (-5)  /* a HIP runtime call failed                                   */
-#define ICRC_ETIMEDOUT (-110) /* a host message's job was not done within the ring's watchdog (2 s) */
+#define ICRC_ETIMEDOUT (-110) /* a submission ring's kernel did not stop (icrc_engine_destroy, icrc_shutdown) */
 /* PacketWriter errors (PacketProcessorError, packet_processor.rs:127-148) */
 #define ICRC_EBUFFER_NOT_LARGE (-1000) /* BufferNotLargeEnough(usize)                     */
 #define ICRC_ELENGTH_TOO_LONG (-1001)  /* LengthTooLong(usize)                            */
@@ -99,7 +100,17 @@ int icrc_abi_check(uint32_t abi_version, size_t write_msg_bytes, size_t rx_desc_
 /* One engine per GPU: owns the LDS table images in HBM (160 KiB each, plus a 36 KiB compact form the
  * kernels replicate into LDS), a stream and staging. */
 int icrc_engine_create(int device, icrc_engine **out);
+/* ICRC_EINVAL for a handle that is not a live engine (NULL, destroyed, or gone with icrc_shutdown).
+ * ICRC_ETIMEDOUT when the engine's submission ring kernel did not stop within 1 s: the engine is
+ * gone, but the ring's stream and memory are left in place (never waited for). */
 int icrc_engine_destroy(icrc_engine *engine);
+/* Process teardown, before the HIP runtime's own: stops every submission ring, synchronises and
+ * destroys every engine (the default ones and those from icrc_engine_create: their handles become
+ * invalid) and frees every thread's staging slot.  Afterwards no entry point makes a HIP call: those
+ * that need the GPU return ICRC_EDEVICE (engines) / ICRC_ENODEV, icrc_device_count returns 0.  Call
+ * it from the host program's exit path (the Python binding registers it with atexit).  Returns
+ * ICRC_OK, or ICRC_ETIMEDOUT when a ring kernel did not stop (left in place, as above).  Idempotent. */
+int icrc_shutdown(void);
 /* Lazily created, lock-protected default engine for `device` (-1 = current HIP device). */
 int icrc_engine_default(int device, icrc_engine **out);
 int icrc_engine_device_ordinal(const icrc_engine *engine);
@@ -435,6 +446,9 @@ int icrc_rdma_header_len(uint8_t opcode);
 int icrc_table_image(uint32_t *out_words, uint32_t nwords);
 /* The oct kernel's image (eight packets per wavefront): M^8 bulk, M^(8 - (l & 7)) final. */
 int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords);
+/* Removed in ABI 5 with the quad kernels; still exported (one release) so that old dynamic links
+ * resolve.  Always returns ICRC_EINVAL. */
+int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords);
 
 #ifdef __cplusplus
 }

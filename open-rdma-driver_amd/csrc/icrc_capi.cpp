@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -131,7 +132,7 @@ struct icrc_engine {
     Stage st[2];
     std::mutex comb_init_mu;
     std::unique_ptr<Combiner> comb;  // scalar calls (created on first use)
-    int host_path = ICRC_HOST_RING;  // scalar calls and host messages: the submission ring or launches
+    std::atomic<int> host_path{ICRC_HOST_RING};  // scalar calls and host messages: the submission ring or launches
     std::mutex ring_mu;
     std::unique_ptr<struct RingState> ring;  // the submission ring (created on first use)
 };
@@ -140,10 +141,27 @@ namespace {
 
 using icrc::BatchParams;
 
+// icrc_shutdown (include/icrc.h) has run: every engine is gone and no entry point makes a HIP call
+// any more (DeviceGuard refuses, the scalar / default-engine paths check first).  Counted refusals are
+// the teardown test's evidence (icrc_teardown_stats).
+std::atomic<bool> g_shutdown{false};
+std::atomic<uint64_t> g_refused_after_shutdown{0};
+std::atomic<uint64_t> g_engines_torn_down{0};
+std::atomic<uint64_t> g_slots_freed_at_shutdown{0};
+bool shut_down() {
+    if (!g_shutdown.load(std::memory_order_acquire)) return false;
+    g_refused_after_shutdown.fetch_add(1, std::memory_order_relaxed);
+    return true;
+}
+
 struct DeviceGuard {
     int prev = -1;
     bool ok = true;
     explicit DeviceGuard(int dev) {
+        if (shut_down()) {  // no HIP call after icrc_shutdown
+            ok = false;
+            return;
+        }
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
     }
@@ -259,9 +277,40 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     return rc;
 }
 
+// The CUs a device batch can have: all of them, less those the engine's submission ring holds while
+// its service kernel is resident (one 160 KiB-LDS workgroup per CU, 32 by default).  Every batch
+// kernel is a persistent grid of one workgroup per CU with a fixed share per workgroup: a grid that
+// counted the ring's CUs would leave those workgroups queued until the ring's kernel ends (up to its
+// 1 ms lifetime) and the whole batch would wait for them.
+// Live rings (every engine's, with its device), never destroyed: read by device dispatch (free_cus)
+// and stopped at process exit if icrc_shutdown never ran (ring_atexit).
+struct RingEntry {
+    int device;
+    icrc::HostRing *ring;
+};
+std::mutex g_ring_mu;
+std::vector<RingEntry> &g_rings = *new std::vector<RingEntry>();
+
+int free_cus(const icrc_engine *e) {
+#ifdef ICRC_AB_BUILD
+    static const bool aware = [] {
+        const char *v = std::getenv("ICRC_AB_RING_AWARE");
+        return !v || std::atoi(v) != 0;
+    }();
+    if (!aware) return e->num_cu;
+#endif
+    int held = 0;  // any engine's ring on this device (the default engine's, an Engine's of its own)
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        for (const RingEntry &r : g_rings)
+            if (r.device == e->device && r.ring->live()) held += static_cast<int>(r.ring->workgroups());
+    }
+    return held < e->num_cu ? e->num_cu - held : e->num_cu;
+}
+
 int grid_for(const icrc_engine *e, uint32_t n) {
     const uint64_t want = (static_cast<uint64_t>(n) + icrc::kWavesPerGroup - 1) / icrc::kWavesPerGroup;
-    return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(want, static_cast<uint64_t>(e->num_cu))));
+    return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(want, static_cast<uint64_t>(free_cus(e)))));
 }
 
 void stage_free(Stage &s) {
@@ -333,8 +382,12 @@ bool host_pinned(const void *p) {
     return a.type == hipMemoryTypeHost;
 }
 
-std::mutex g_registry_mu;
-std::map<int, icrc_engine *> g_default;
+// Engine registries, never destroyed (a thread or handler running after static destruction must not
+// find them gone): every live engine (icrc_engine_destroy refuses one it does not hold, so a handle
+// destroyed by icrc_shutdown and then by its owner is not freed twice) and the default engines.
+std::recursive_mutex g_registry_mu;  // recursive: icrc_engine_default creates under it
+std::map<int, icrc_engine *> &g_default = *new std::map<int, icrc_engine *>();
+std::set<icrc_engine *> &g_engines = *new std::set<icrc_engine *>();
 
 int validate_host(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint32_t n) {
     if (n == 0) return ICRC_OK;
@@ -594,13 +647,26 @@ int device_batch(icrc_engine *e, int mode, uint8_t *d_base, const uint64_t *d_of
 // Per-thread pinned, device-mapped staging: each calling thread copies its packets into a slot of
 // its own (no lock around the copy); the slot outlives the call, one per (thread, engine), and
 // grows to the largest call the thread has made.
+// Every slot's pinned block is also listed in g_slots: icrc_shutdown frees them all (threads that
+// never exit, the main thread's slot) while the runtime is alive, and a slot whose block shutdown
+// already freed makes no HIP call from its thread-exit destructor.
+std::mutex g_slot_mu;
+std::set<void *> &g_slots = *new std::set<void *>();
+void slot_block_free(void *h) {
+    bool mine = false;
+    {
+        std::lock_guard<std::mutex> lk(g_slot_mu);
+        mine = g_slots.erase(h) != 0;
+    }
+    if (mine) (void)hipHostFree(h);
+}
 struct StageSlot {
     const icrc_engine *engine = nullptr;
     uint8_t *h = nullptr;  // pinned host
     uint8_t *d = nullptr;  // device view
     size_t cap = 0;
     ~StageSlot() {
-        if (h) (void)hipHostFree(h);
+        if (h) slot_block_free(h);
     }
 };
 constexpr size_t kScalarSlotBytes = 65536 + 64;  // any packet the C-ABI accepts (len <= 65535)
@@ -615,14 +681,20 @@ thread_local StageSlot t_slot;
 int stage_slot(const icrc_engine *e, size_t bytes, uint8_t **h, uint8_t **d) {
     bytes = std::max(bytes, kScalarSlotBytes);
     if (t_slot.engine != e || !t_slot.h || t_slot.cap < bytes) {
-        if (t_slot.h) (void)hipHostFree(t_slot.h);
-        t_slot = StageSlot{};
+        if (t_slot.h) slot_block_free(t_slot.h);
+        t_slot.engine = nullptr;
+        t_slot.h = t_slot.d = nullptr;
+        t_slot.cap = 0;
         void *p = nullptr;
         if (hipHostMalloc(&p, bytes, hipHostMallocMapped) != hipSuccess) return ICRC_ENOMEM;
         void *dp = nullptr;
         if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
             (void)hipHostFree(p);
             return ICRC_EDEVICE;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_slot_mu);
+            g_slots.insert(p);
         }
         t_slot.engine = e;
         t_slot.h = static_cast<uint8_t *>(p);
@@ -784,8 +856,6 @@ int RingHip::ended() {
 
 // Live rings, stopped at process exit: every wave ends (host memory only, no HIP call) before the
 // runtime's own teardown, which registered its handlers before ours.
-std::mutex g_ring_mu;
-std::vector<icrc::HostRing *> g_rings;
 #ifdef ICRC_AB_BUILD
 // ICRC_RING_TRACE (A/B library): per-slot job stamps from the ring kernel, summarised at exit
 struct RingTrace {
@@ -820,27 +890,39 @@ void ring_trace_dump() {
 }
 #endif
 
+// The last resort for a C caller that never calls icrc_shutdown: the rings' waves are stopped through
+// host memory only (no HIP call).  Python's binding calls icrc_shutdown from its own atexit handler,
+// before the interpreter and the HIP runtime finalise, and this then finds no ring.
 void ring_atexit() {
     std::lock_guard<std::mutex> lk(g_ring_mu);
-    for (icrc::HostRing *r : g_rings) (void)r->stop(1000000);
+    for (const RingEntry &r : g_rings) (void)r.ring->stop(1000000);
 #ifdef ICRC_AB_BUILD
     ring_trace_dump();
 #endif
 }
 
-void ring_free(icrc_engine *e) {
+int ring_free(icrc_engine *e) {
     std::unique_ptr<RingState> rs;
     {
         std::lock_guard<std::mutex> lk(e->ring_mu);
         rs = std::move(e->ring);
     }
-    if (!rs) return;
+    if (!rs) return ICRC_OK;
     if (rs->ring) {
         {
             std::lock_guard<std::mutex> lk(g_ring_mu);
-            g_rings.erase(std::remove(g_rings.begin(), g_rings.end(), rs->ring.get()), g_rings.end());
+            const icrc::HostRing *mine = rs->ring.get();
+            g_rings.erase(std::remove_if(g_rings.begin(), g_rings.end(), [&](const RingEntry &x) { return x.ring == mine; }),
+                          g_rings.end());
         }
-        (void)rs->ring->stop(1000000);
+        if (rs->ring->stop(1000000) != ICRC_OK) {
+            // a wedged service kernel (the case in which the watchdog retired the ring): neither wait
+            // for its stream nor free memory its waves may still touch.  The ring is leaked.
+            std::fprintf(stderr, "icrc_amd: the submission ring's kernel did not stop within 1 s; its stream and "
+                                 "memory are left in place\n");
+            (void)rs.release();
+            return ICRC_ETIMEDOUT;
+        }
     }
     if (rs->dev.stream) {
         (void)hipStreamSynchronize(rs->dev.stream);
@@ -848,6 +930,7 @@ void ring_free(icrc_engine *e) {
     }
     if (rs->d_mem) (void)hipFree(rs->d_mem);
     if (rs->host) (void)hipHostFree(rs->host);
+    return ICRC_OK;
 }
 
 // The engine's ring, created on first use (nullptr, with *rc, when it cannot be: the caller falls
@@ -946,12 +1029,15 @@ icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
         }
     }
 #endif
-    r->ring = std::make_unique<icrc::HostRing>(&r->dev, mem, nslots, wgs, kRingWatchdogUs);
+    uint64_t watchdog_us = kRingWatchdogUs;
+    if (const char *v = std::getenv("ICRC_RING_WATCHDOG_US"))  // test knob: the watchdog's fallback path
+        watchdog_us = static_cast<uint64_t>(std::max(1, std::min(2000000, std::atoi(v))));
+    r->ring = std::make_unique<icrc::HostRing>(&r->dev, mem, nslots, wgs, watchdog_us);
     {
         static std::once_flag once;
         std::call_once(once, [] { std::atexit(ring_atexit); });
         std::lock_guard<std::mutex> gl(g_ring_mu);
-        g_rings.push_back(r->ring.get());
+        g_rings.push_back(RingEntry{e->device, r->ring.get()});
     }
     *rc = ICRC_OK;
     return r->ring.get();
@@ -960,11 +1046,12 @@ icrc::HostRing *ring_for(icrc_engine *e, int *rc) {
 // One host message (n packets at dbase, the device view of pinned host memory; off / len host
 // arrays relative to dbase) -> n ICRCs into res: through the submission ring, or (host path
 // ICRC_HOST_LAUNCH, or a ring that cannot run) one launch through the four-lane submitter.  A
-// ring watchdog timeout fails the call (ICRC_ETIMEDOUT).
+// ring watchdog timeout retires the ring and the call runs as a launch (a GPU whose CUs
+// are all held by other work would otherwise fail a valid call); a stopped ring fails the call.
 int host_job(icrc_engine *e, const uint8_t *dbase, const uint64_t *off, const uint32_t *len, uint32_t n,
              uint32_t *res) {
     int rc = ICRC_OK;
-    if (e->host_path == ICRC_HOST_RING && n <= icrc::kRingMaxPackets) {
+    if (e->host_path.load(std::memory_order_relaxed) == ICRC_HOST_RING && n <= icrc::kRingMaxPackets) {
         icrc::HostRing *ring = ring_for(e, &rc);
         if (ring && !ring->retired()) {
             icrc::RingJob j;
@@ -984,7 +1071,13 @@ int host_job(icrc_engine *e, const uint8_t *dbase, const uint64_t *off, const ui
                 j.len = len;
             }
             rc = ring->submit(j);
-            if (rc != ICRC_EDEVICE) return rc;  // done, or the watchdog: the call fails
+            if (rc == ICRC_OK) return rc;
+            // a stopped ring (engine destruction, process exit): no launch either
+            if (ring->stopped()) return ICRC_EDEVICE;
+            // the watchdog (ICRC_ETIMEDOUT: counted in host_stats, the slot stays quarantined with its
+            // own result array, the ring is retired) or a failed launch: this call runs as a launch
+        } else if (ring && ring->stopped()) {
+            return ICRC_EDEVICE;
         }
     }
     Combiner *c = combiner(e, &rc);
@@ -1095,6 +1188,28 @@ int message_batch(icrc_engine *e, int mode, uint8_t *base, const uint64_t *off, 
     return ICRC_OK;
 }
 
+// Everything an engine holds on the device, in dependency order (no registry work: the callers,
+// icrc_engine_destroy and icrc_shutdown, have already taken the engine out of the registries).  The
+// HIP calls here run before the runtime's teardown: from the caller, or from icrc_shutdown.
+int engine_teardown(icrc_engine *e) {
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != e->device) (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->side) (void)hipStreamSynchronize(e->side);
+    const int rc = ring_free(e);
+    for (Stage &s : e->st) stage_free(s);
+    combiner_free(e);
+    if (e->d_table) (void)hipFree(e->d_table);
+    if (e->d_table_oct) (void)hipFree(e->d_table_oct);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->side) (void)hipStreamDestroy(e->side);
+    if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+    if (e->join_ev) (void)hipEventDestroy(e->join_ev);
+    if (prev >= 0 && prev != e->device) (void)hipSetDevice(prev);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1125,7 +1240,7 @@ int icrc_abi_check(uint32_t abi_version, size_t write_msg_bytes, size_t rx_desc_
 
 int icrc_engine_set_host_path(icrc_engine *e, int path) {
     if (!e || (path != ICRC_HOST_RING && path != ICRC_HOST_LAUNCH)) return ICRC_EINVAL;
-    e->host_path = path;
+    e->host_path.store(path, std::memory_order_relaxed);
     return ICRC_OK;
 }
 
@@ -1144,6 +1259,7 @@ int icrc_engine_host_stats(icrc_engine *e, uint64_t out[4]) {
 }
 
 int icrc_device_count(void) {
+    if (shut_down()) return 0;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
@@ -1152,6 +1268,7 @@ int icrc_device_count(void) {
 int icrc_engine_create(int device, icrc_engine **out) {
     if (!out) return ICRC_EINVAL;
     *out = nullptr;
+    if (shut_down()) return ICRC_EDEVICE;
     int ndev = icrc_device_count();
     if (ndev <= 0) return ICRC_ENODEV;
     if (device < 0) {
@@ -1184,8 +1301,18 @@ int icrc_engine_create(int device, icrc_engine **out) {
         hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess) {
-        icrc_engine_destroy(e);
+        (void)engine_teardown(e);
+        delete e;
         return ICRC_EDEVICE;
+    }
+    {
+        std::lock_guard<std::recursive_mutex> lk(g_registry_mu);
+        if (g_shutdown.load(std::memory_order_acquire)) {  // icrc_shutdown ran meanwhile
+            (void)engine_teardown(e);
+            delete e;
+            return ICRC_EDEVICE;
+        }
+        g_engines.insert(e);
     }
     *out = e;
     return ICRC_OK;
@@ -1194,38 +1321,54 @@ int icrc_engine_create(int device, icrc_engine **out) {
 int icrc_engine_destroy(icrc_engine *e) {
     if (!e) return ICRC_EINVAL;
     {
-        DeviceGuard g(e->device);
-        if (e->stream) (void)hipStreamSynchronize(e->stream);
-        if (e->side) (void)hipStreamSynchronize(e->side);
-        ring_free(e);
-        for (Stage &s : e->st) stage_free(s);
-        combiner_free(e);
-        if (e->d_table) (void)hipFree(e->d_table);
-        if (e->d_table_oct) (void)hipFree(e->d_table_oct);
-        if (e->stream) (void)hipStreamDestroy(e->stream);
-        if (e->side) (void)hipStreamDestroy(e->side);
-        if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
-        if (e->join_ev) (void)hipEventDestroy(e->join_ev);
-    }
-    {
-        std::lock_guard<std::mutex> lk(g_registry_mu);
+        std::lock_guard<std::recursive_mutex> lk(g_registry_mu);
+        if (g_engines.erase(e) == 0) return ICRC_EINVAL;  // not live: destroyed, or gone with icrc_shutdown
         for (auto it = g_default.begin(); it != g_default.end(); ++it)
             if (it->second == e) {
                 g_default.erase(it);
                 break;
             }
     }
+    const int rc = engine_teardown(e);
     delete e;
-    return ICRC_OK;
+    return rc;
+}
+
+int icrc_shutdown(void) {
+    std::vector<icrc_engine *> live;
+    {
+        std::lock_guard<std::recursive_mutex> lk(g_registry_mu);
+        if (g_shutdown.exchange(true, std::memory_order_acq_rel)) return ICRC_OK;  // idempotent
+        live.assign(g_engines.begin(), g_engines.end());
+        g_engines.clear();
+        g_default.clear();
+    }
+    int rc = ICRC_OK;
+    for (icrc_engine *e : live) {
+        const int r = engine_teardown(e);
+        if (rc == ICRC_OK) rc = r;
+        delete e;
+        g_engines_torn_down.fetch_add(1, std::memory_order_relaxed);
+    }
+    std::vector<void *> slots;
+    {
+        std::lock_guard<std::mutex> lk(g_slot_mu);
+        slots.assign(g_slots.begin(), g_slots.end());
+        g_slots.clear();
+    }
+    for (void *h : slots) (void)hipHostFree(h);
+    g_slots_freed_at_shutdown.fetch_add(slots.size(), std::memory_order_relaxed);
+    return rc;
 }
 
 int icrc_engine_default(int device, icrc_engine **out) {
     if (!out) return ICRC_EINVAL;
+    if (shut_down()) return ICRC_EDEVICE;
     if (device < 0) {
         if (icrc_device_count() <= 0) return ICRC_ENODEV;
         if (hipGetDevice(&device) != hipSuccess) device = 0;
     }
-    std::lock_guard<std::mutex> lk(g_registry_mu);
+    std::lock_guard<std::recursive_mutex> lk(g_registry_mu);
     auto it = g_default.find(device);
     if (it != g_default.end()) {
         *out = it->second;
@@ -1512,7 +1655,27 @@ int icrc_table_image_oct(uint32_t *out_words, uint32_t nwords) {
     return ICRC_OK;
 }
 
+// Removed in ABI 5 (the quad kernels were retired in round 5); kept exported for one release so that
+// an existing dynamic link still resolves.  Always ICRC_EINVAL.
+int icrc_table_image_quad(uint32_t *out_words, uint32_t nwords) {
+    (void)out_words;
+    (void)nwords;
+    return ICRC_EINVAL;
+}
+
 }  // extern "C"
+
+// Test hook (not in include/icrc.h): the teardown's record.  out[0] 1 once icrc_shutdown has run,
+// [1] engines it destroyed, [2] staging slots it freed, [3] entry points refused afterwards (each of
+// them returned before any HIP call).
+extern "C" int icrc_teardown_stats(uint64_t out[4]) {
+    if (!out) return ICRC_EINVAL;
+    out[0] = g_shutdown.load(std::memory_order_acquire) ? 1u : 0u;
+    out[1] = g_engines_torn_down.load(std::memory_order_relaxed);
+    out[2] = g_slots_freed_at_shutdown.load(std::memory_order_relaxed);
+    out[3] = g_refused_after_shutdown.load(std::memory_order_relaxed);
+    return ICRC_OK;
+}
 
 // Test hook (not in include/icrc.h): `threads` callers each run `jobs` copy-pool jobs of 1..300
 // tasks at once; every task of every job must run exactly once and each job must return only

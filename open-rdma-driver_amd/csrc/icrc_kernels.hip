@@ -725,6 +725,36 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
     }
 }
 
+#ifdef ICRC_AB_BUILD
+// A/B: the fixed cost of a small-batch launch (configs[3]: 4096 packets, one per wave), decomposed
+// (VERDICT r05 item 2).  Same grid, block and LDS size as icrc_batch_kernel; each wave stores one
+// result per packet of its one-packet range (as the batch kernel's final store) and nothing else:
+//   CUT 0 (variant 24) the launch alone (waves start, the LDS image is allocated, one store);
+//   CUT 1 (25) + the table image into LDS (table_fetch / table_store, the barrier);
+//   CUT 2 (26) + each wave's (offset, length) load before the table wait (a ragged batch's meta).
+template <int MODE, int CUT>
+__global__ __launch_bounds__(kThreadsPerGroup) void icrc_fixed_cost_kernel(BatchParams p) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t gw = blockIdx.x * kWavesPerGroup + wave;
+    uint32_t v = gw;
+    if constexpr (CUT >= 2) {
+        if (gw < p.n) v ^= static_cast<uint32_t>(p.off ? p.off[gw] : gw * p.stride) ^ (p.len ? p.len[gw] : p.ulen);
+    }
+    if constexpr (CUT >= 1) {
+        table_fill(lds4, p.table);
+        v ^= reinterpret_cast<const uint32_t *>(lds4)[lane * 33u];
+    } else if (p.n == 0xFFFFFFFFu) {  // never taken: keeps the LDS image allocated
+        lds4[threadIdx.x] = make_uint4(v, v, v, v);
+        __syncthreads();
+        v ^= reinterpret_cast<const uint32_t *>(lds4)[lane * 33u];
+    }
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (lane == 0 && gw < p.n) store_result<MODE>(p, gw, v);
+}
+#endif
+
 }  // namespace
 
 #define ICRC_LAUNCH(S, D, A, T) \
@@ -763,6 +793,9 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 21: ICRC_LAUNCH(2, 1, RingNoFinal, false); break;   // 16 without final products
     case 22: ICRC_LAUNCH(2, 1, RingNoStore, false); break;   // 16 without result stores
     case 23: ICRC_LAUNCH(2, 1, RingBare, false); break;      // 19 without final products and stores
+    case 24: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 0>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 25: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 26: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products

@@ -157,6 +157,7 @@ int HostRing::submit(const RingJob &j) {
 }
 
 int HostRing::stop(uint64_t wait_us) {
+    stopped_.store(true, std::memory_order_release);
     retired_.store(true, std::memory_order_release);
     slot_cv_.notify_all();
     std::lock_guard<std::mutex> lk(launch_mu_);

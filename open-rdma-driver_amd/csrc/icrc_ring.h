@@ -52,7 +52,7 @@ struct RingStats {
 class HostRing {
    public:
     // watchdog_us: a job not done after this long fails with ICRC_ETIMEDOUT and the ring is
-    // retired (the caller falls back to kernel launches).
+    // retired (the caller runs the job, and later ones, as kernel launches).
     HostRing(RingDevice *dev, const RingMemory &mem, uint32_t nslots, uint32_t wg_per_slot, uint64_t watchdog_us);
     // Runs one job.  ICRC_OK; ICRC_EINVAL (n == 0 or > kRingMaxPackets); ICRC_ETIMEDOUT (watchdog);
     // ICRC_EDEVICE (launch failed, or the ring was retired).
@@ -61,8 +61,15 @@ class HostRing {
     // of the current launch has stored its exited word, or wait_us.  Returns ICRC_OK or ICRC_ETIMEDOUT.
     int stop(uint64_t wait_us);
     bool retired() const { return retired_.load(std::memory_order_acquire); }
+    // stop() has been called (engine destruction, process exit): unlike a ring retired by its
+    // watchdog, callers must not fall back to kernel launches.
+    bool stopped() const { return stopped_.load(std::memory_order_acquire); }
     RingStats stats() const;
     uint32_t epoch() const { return epoch_; }
+    // A hint for device dispatch (no lock, no device call): an instance of the service kernel has
+    // been launched and its workgroups have not all ended, so they hold their CUs.
+    bool live() const { return launched_.load(std::memory_order_acquire) && !launch_ended(); }
+    uint32_t workgroups() const { return nslots_ * wg_per_slot_; }
     uint32_t words_per_slot() const { return wps_; }
 
    private:
@@ -81,9 +88,10 @@ class HostRing {
     uint32_t free_mask_;
     uint32_t seq_[kRingMaxSlots] = {};
     std::mutex launch_mu_;
-    uint32_t epoch_ = 0;
-    bool launched_ = false;
+    std::atomic<uint32_t> epoch_{0};
+    std::atomic<bool> launched_{false};
     std::atomic<bool> retired_{false};
+    std::atomic<bool> stopped_{false};
     std::atomic<uint32_t> activity_{0};
     mutable std::mutex stats_mu_;
     RingStats stats_;

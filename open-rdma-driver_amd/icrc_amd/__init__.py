@@ -14,9 +14,11 @@ with no GPU every compute call raises IcrcError(ENODEV).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import ipaddress
 import os
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -179,6 +181,8 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
         "icrc_abi_check": (i32, [u32, sz, sz, sz, sz]),
         "icrc_engine_set_host_path": (i32, [vp, i32]),
         "icrc_engine_host_stats": (i32, [vp, ctypes.POINTER(u64)]),
+        "icrc_shutdown": (i32, []),
+        "icrc_teardown_stats": (i32, [ctypes.POINTER(u64)]),  # test hook, not in include/icrc.h
         "icrc_ring_selftest": (i32, [i32, i32, i32]),  # test hook, not in include/icrc.h
         "icrc_copy_pool_selftest": (i32, [i32, i32]),  # test hook, not in include/icrc.h
     }
@@ -191,6 +195,34 @@ def _load(path: str = LIB_PATH) -> ctypes.CDLL:
 
 lib = _load()
 _ab_lib = None
+_live_engines: "weakref.WeakSet[Engine]" = weakref.WeakSet()
+
+
+def _shutdown() -> None:
+    """atexit: deterministic teardown before the interpreter, torch and the HIP runtime finalise
+    (VERDICT r05 item 1).  Every Engine still open is closed, then icrc_shutdown stops the default
+    engines' submission rings, destroys the engines and frees every thread's staging slot, in each
+    library loaded; afterwards the library makes no HIP call.  Registered at import: Python runs
+    atexit handlers last-in first-out, so this runs before those of modules imported earlier
+    (torch)."""
+    for eng in list(_live_engines):
+        try:
+            eng.close()
+        except Exception:
+            pass
+    for L in (lib, _ab_lib):
+        if L is not None:
+            L.icrc_shutdown()
+
+
+atexit.register(_shutdown)
+
+
+def teardown_stats(L: Optional[ctypes.CDLL] = None) -> dict:
+    """The library's teardown record (icrc_teardown_stats, a test hook)."""
+    out = (ctypes.c_uint64 * 4)()
+    _check((L or lib).icrc_teardown_stats(out), "icrc_teardown_stats")
+    return {"shutdown": out[0], "engines_destroyed": out[1], "slots_freed": out[2], "refused_after": out[3]}
 
 
 def ab_library() -> ctypes.CDLL:
@@ -423,6 +455,7 @@ class Engine:
         self.handle = h
         self.device = device
         self.stream = self._lib.icrc_engine_stream(h) or 0
+        _live_engines.add(self)
 
     @property
     def ordinal(self) -> int:
@@ -444,9 +477,11 @@ class Engine:
         _check(self._lib.icrc_engine_set_kernel_variant(self.handle, variant), "set_kernel_variant")
 
     def close(self) -> None:
+        """icrc_engine_destroy (idempotent; after icrc_shutdown the library has already destroyed it
+        and refuses the handle with EINVAL)."""
         if self.handle:
-            self._lib.icrc_engine_destroy(self.handle)
-            self.handle = None
+            h, self.handle = self.handle, None
+            self._lib.icrc_engine_destroy(h)
 
     def __del__(self):
         try:

@@ -481,6 +481,17 @@ int oracle_rx_parse(uint8_t *pkt, uint32_t len, uint64_t off, int zero_trailer, 
     return ORACLE_OK;
 }
 
+/* oracle_rx_parse over a ragged batch (packet i at base + off[i], len[i] bytes): the same per-packet
+ * restatement, looped here so that a million-packet check costs no per-packet call from Python. */
+int oracle_rx_parse_batch(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n, int zero_trailer,
+                          oracle_rx_desc *out) {
+    for (uint64_t i = 0; i < n; i++) {
+        const int rc = oracle_rx_parse(base + off[i], len[i], off[i], zero_trailer, out + i);
+        if (rc != ORACLE_OK) return rc;
+    }
+    return ORACLE_OK;
+}
+
 /* ---------------------------------------------------------------------------------- */
 /* Synthetic workloads                                                                 */
 /* ---------------------------------------------------------------------------------- */

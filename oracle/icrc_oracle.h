@@ -140,6 +140,8 @@ typedef struct oracle_rx_desc {
 /* pkt = the IPv4 packet at byte offset `off` of the caller's buffer; zero_trailer as
  * is_icrc_valid.  Fills *d; returns 0. */
 int oracle_rx_parse(uint8_t *pkt, uint32_t len, uint64_t off, int zero_trailer, oracle_rx_desc *d);
+int oracle_rx_parse_batch(uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t n, int zero_trailer,
+                          oracle_rx_desc *out);
 
 /* --- Synthetic workloads ----------------------------------------------- */
 uint64_t oracle_mix64(uint64_t x);

@@ -139,6 +139,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_header_len.restype = ctypes.c_int
         L.oracle_rx_parse.argtypes = [u8p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, u8p]
         L.oracle_rx_parse.restype = ctypes.c_int
+        L.oracle_rx_parse_batch.argtypes = [u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_int, u8p]
+        L.oracle_rx_parse_batch.restype = ctypes.c_int
         L.oracle_synth_write.argtypes = [
             u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -304,16 +306,16 @@ assert RX_DESC_DTYPE.itemsize == 72
 
 def rx_parse(base: np.ndarray, off, lens, zero_trailer: bool = False) -> np.ndarray:
     """is_icrc_valid + to_rdma_message(pkt[28 .. L-4)) per packet (icrc_oracle.c
-    oracle_rx_parse); `base` is modified only when zero_trailer."""
-    off = np.asarray(off, np.uint64)
-    lens = np.asarray(lens, np.uint32)
+    oracle_rx_parse, looped in C by oracle_rx_parse_batch); `base` is modified only when
+    zero_trailer."""
+    off = np.ascontiguousarray(off, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
     out = np.zeros(off.size, dtype=RX_DESC_DTYPE)
-    for i in range(off.size):
-        o, L = int(off[i]), int(lens[i])
-        if L < 44:
-            out[i]["icrc_ok"], out[i]["status"] = 0xFF, 3
-            continue
-        lib().oracle_rx_parse(_ptr(base) + o, L, o, 1 if zero_trailer else 0, out[i:i + 1].ctypes.data)
+    if off.size:
+        rc = lib().oracle_rx_parse_batch(_ptr(base), off.ctypes.data, lens.ctypes.data, off.size,
+                                         1 if zero_trailer else 0, out.ctypes.data)
+        if rc != 0:
+            raise ValueError(f"oracle_rx_parse_batch: {rc}")
     return out
 
 

@@ -187,16 +187,20 @@ int main(int argc, char **argv) {
     }
     std::memcpy(pinned, pageable.data(), pageable.size());
     if (argc > 2) {  // msg_probe CALLS THREADS...: the multi-threaded message rate only
+        // MSG_PROBE_KINDS=pinned (bench.py's default-line leg): the pinned buffers alone
+        const char *kinds = getenv("MSG_PROBE_KINDS");
+        const bool all = !kinds || strcmp(kinds, "pinned") != 0;
         for (int a = 2; a < argc; ++a) {
             const int T = atoi(argv[a]);
             run_threads(launch ? "pinned, launch" : "pinned, ring", pageable, 1, npk, L, calls, T);
+            if (!all) continue;
             run_threads(launch ? "pinned_coherent, launch" : "pinned_coherent, ring", pageable, 2, npk, L, calls, T);
             run_threads(launch ? "registered_huge, launch" : "registered_huge, ring", pageable, 3, npk, L, calls, T);
             run_threads(launch ? "pageable, launch" : "pageable, ring", pageable, 0, npk, L, calls, T);
         }
         print_stats(path);
         (void)hipHostFree(pinned);
-        return 0;
+        return icrc_shutdown() == ICRC_OK ? 0 : 1;  // the ring and engine go before the HIP runtime's teardown
     }
     run(launch ? "pinned, launch" : "pinned, ring", pinned, npk, L, calls);
     run(launch ? "pageable, launch" : "pageable, ring", pageable.data(), npk, L, calls);
@@ -204,5 +208,5 @@ int main(int argc, char **argv) {
     run(launch ? "pageable_1_packet, launch" : "pageable_1_packet, ring", pageable.data(), 1, L, calls);
     print_stats(path);
     (void)hipHostFree(pinned);
-    return 0;
+    return icrc_shutdown() == ICRC_OK ? 0 : 1;
 }

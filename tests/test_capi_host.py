@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     import icrc_amd
 
     names = declared_functions()
-    assert len(names) == 35, names
+    assert len(names) == 37, names
     missing = [n for n in names if not hasattr(ctypes.CDLL(icrc_amd.LIB_PATH), n)]
     assert not missing, missing
 
@@ -58,6 +58,52 @@ def test_submission_ring_protocol(scenario, what):
     import icrc_amd
 
     assert icrc_amd.ring_selftest(scenario, 3, 150) == 0, what
+
+
+TEARDOWN_SCRIPT = """
+import atexit, ctypes, json, sys
+sys.path[:0] = {paths!r}
+
+def report():  # registered before icrc_amd is imported: runs after the binding's atexit teardown
+    import icrc_amd
+    before = icrc_amd.teardown_stats()
+    err = ctypes.c_int(0)
+    buf = (ctypes.c_uint8 * 64)()
+    icrc_amd.lib.icrc_compute(buf, 64, ctypes.byref(err))
+    h = ctypes.c_void_p()
+    rc_default = icrc_amd.lib.icrc_engine_default(-1, ctypes.byref(h))
+    print(json.dumps({{"before": before, "after": icrc_amd.teardown_stats(), "err": err.value,
+                      "default": rc_default, "devices": icrc_amd.lib.icrc_device_count(),
+                      "second": icrc_amd.lib.icrc_shutdown()}}))
+
+atexit.register(report)
+import icrc_amd
+"""
+
+
+def test_teardown_order_at_interpreter_exit(tmp_path):
+    """VERDICT r05 item 1, the order on any machine: importing the binding registers its atexit
+    teardown (close every Engine, then icrc_shutdown); a handler that runs after it finds the library
+    shut down, and every entry point it calls is refused BEFORE any HIP call (counted by the
+    library), so nothing touches HIP or pinned memory from the exit path's later stages.  The GPU
+    form (Python threads through the ring, then exit) is test_gpu_ring.py's."""
+    import json
+    import subprocess
+    import sys
+
+    import icrc_amd
+
+    paths = [os.path.join(ROOT, "open-rdma-driver_amd"), os.path.join(ROOT, "oracle")]
+    script = tmp_path / "teardown.py"
+    script.write_text(TEARDOWN_SCRIPT.format(paths=paths))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    b, a = rec["before"], rec["after"]
+    assert b["shutdown"] == 1, rec
+    assert rec["err"] == icrc_amd.EDEVICE and rec["default"] == icrc_amd.EDEVICE and rec["devices"] == 0, rec
+    assert a["refused_after"] >= b["refused_after"] + 2, rec  # icrc_compute, icrc_engine_default
+    assert rec["second"] == icrc_amd.OK  # idempotent
 
 
 def test_library_is_gfx950_hip_code():

@@ -966,6 +966,48 @@ def test_rx_parse_ragged_one_pass(engine, zero_trailer):
     assert int(np.sum(want["status"] == 0)) > n // 2 and int(np.sum(want["icrc_ok"] == 0)) >= n // 29
 
 
+def test_rx_parse_mixed_mtu_stream_full(engine):
+    """the receive parse on the emulator's mixed-MTU batch itself (configs[2]'s
+    generator, mixed_mtu_stream: 256 B / 1 KiB / 4 KiB MTU classes, power law, 10 % ragged LAST
+    packets) at 1 Mi packets — the default ragged dispatch (the one-pass ragged ring, the long-packet
+    verify and the sweep) against the oracle, every descriptor and ok byte, with one flipped ICRC per
+    97 packets; then the same batch with zero_trailer."""
+    import icrc_amd
+    from icrc_amd import workloads
+
+    wm = workloads.mixed_mtu_stream(1 << 20, seed=77)
+    s = stream_handle()
+    d_buf = workloads.synthesize(engine, wm, stream=s)
+    torch.cuda.synchronize()
+    buf = d_buf.cpu().numpy()
+    del d_buf
+    off, lens = np.ascontiguousarray(wm.off, np.uint64), np.ascontiguousarray(wm.lens, np.uint32)
+    ic = oracle.compute_icrc_batch(buf, off, lens)
+    tr = (off + lens - 4).astype(np.int64)
+    for k in range(4):
+        buf[tr + k] = ((ic >> (8 * k)) & 0xFF).astype(np.uint8)
+    buf[tr[::97]] ^= 0x08
+    for zero_trailer in (False, True):
+        ref = buf.copy()
+        want = oracle.rx_parse(ref, off, lens, zero_trailer=zero_trailer)
+        d_buf = dev(buf)
+        d_off, d_len = dev(off), dev(lens)
+        d_desc = torch.zeros(wm.n * 72, dtype=torch.uint8, device="cuda")
+        d_ok = torch.full((wm.n,), 7, dtype=torch.uint8, device="cuda")
+        engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), wm.n, d_desc.data_ptr(), d_ok.data_ptr(),
+                        zero_trailer=zero_trailer, stream=s)
+        torch.cuda.synchronize()
+        got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+        assert_desc_equal(got, want)
+        np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
+        if zero_trailer:
+            np.testing.assert_array_equal(d_buf.cpu().numpy(), ref)
+        del d_buf, d_off, d_len, d_desc, d_ok
+    assert int(np.sum(want["icrc_ok"] == 0)) == (wm.n + 96) // 97
+    assert np.all(want["status"] == 0)
+    assert len(set(want["payload_len"].tolist())) > 100  # the ragged LAST packets' lengths
+
+
 def test_send_receive_roundtrip(engine):
     """Packetize 24 WRITE / READ RESPONSE messages on the GPU, parse them on the GPU, and place each
     payload at its RETH va: the memory region equals the source bytes (C3 closed on-device)."""

@@ -8,6 +8,11 @@ the results through the ring, that the ring really ran, that it and the launch p
 threads at once (the launch submitter's merge path included), the relaunch after an idle exit, and
 that the resident kernel does not hold back work on other streams.
 """
+import json
+import os
+import subprocess
+import sys
+import textwrap
 import threading
 import time
 
@@ -233,7 +238,8 @@ def test_ring_workgroup_shapes(threads, wgs, monkeypatch):
             host = pinned_copy(ref, keep) if k % 2 else ref.copy()
             np.testing.assert_array_equal(eng.compute_batch_host(host, off, lens, write_trailer=True), want)
             bad = int(rng.integers(0, len(lens)))
-            host[int(off[bad]) + 50] ^= 0x01
+            # a bit inside packet `bad` past its masked header and before its trailer (L >= 44)
+            host[int(off[bad]) + 40 + int(rng.integers(0, int(lens[bad]) - 44 + 1))] ^= 0x01
             ok = eng.verify_batch_host(host, off, lens, zero_trailer=False)
             expect = np.ones(len(lens), np.uint8)
             expect[bad] = 0
@@ -242,3 +248,83 @@ def test_ring_workgroup_shapes(threads, wgs, monkeypatch):
         assert st["jobs"] == 2 * len(cases) and st["timeouts"] == 0, st
     finally:
         eng.close()
+
+
+def test_ring_watchdog_falls_back_to_launch(monkeypatch):
+    """a job the ring does not finish within its watchdog (here 1 us, so the first job
+    always misses it) retires the ring and the call runs as a kernel launch: the result is right,
+    the timeout is counted, and later calls take the launch path (the ring runs no more jobs)."""
+    import icrc_amd
+
+    monkeypatch.setenv("ICRC_RING_WATCHDOG_US", "1")
+    eng = icrc_amd.Engine(0)
+    try:
+        for k in range(3):
+            ref, off, lens = c0_message(6 + k)
+            want = oracle.compute_icrc_batch(ref, np.asarray(off, np.uint64), np.asarray(lens, np.uint32))
+            np.testing.assert_array_equal(eng.compute_batch_host(ref.copy(), off, lens), want)
+        st = eng.host_stats()
+        assert st["timeouts"] == 1 and st["jobs"] == 0, st
+    finally:
+        eng.close()
+
+
+EXIT_SCRIPT = textwrap.dedent("""
+    import atexit, ctypes, json, sys, threading
+    sys.path[:0] = {paths!r}
+    import numpy as np
+    import torch
+
+    def report():  # registered before icrc_amd: runs after the binding's own atexit teardown
+        import icrc_amd
+        before = icrc_amd.teardown_stats()
+        err = ctypes.c_int(0)
+        pkt = np.zeros(64, np.uint8)
+        icrc_amd.lib.icrc_compute(pkt.ctypes.data, pkt.size, ctypes.byref(err))
+        print(json.dumps({{"before": before, "after": icrc_amd.teardown_stats(), "err": err.value,
+                          "devices": icrc_amd.lib.icrc_device_count(), "jobs": JOBS}}), flush=True)
+
+    atexit.register(report)
+    import icrc_amd
+    import oracle
+    JOBS = []
+    buf, off, lens = oracle.synth_write(256 << 10, 4096, local_va=0x7F7E8EE00000, remote_va=0x7F7E8FC00000,
+                                        rkey=3, dqpn=2, psn0=0, msn=0, dst_ip=0xC0A80003, payload_key=0xC0)
+    want = oracle.compute_icrc_batch(buf, off, lens)
+    bad = []
+
+    def worker():
+        b = buf.copy()
+        for _ in range(200):
+            if not np.array_equal(icrc_amd.compute_icrc_batch(b, off, lens), want):
+                bad.append(1)
+
+    ths = [threading.Thread(target=worker) for _ in range(3)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not bad
+    assert icrc_amd.compute_icrc(buf[:4156]) == want[0]  # the main thread's staging slot: freed at teardown
+    JOBS.append(icrc_amd.host_stats()["jobs"])
+    kept_open = icrc_amd.Engine(0)  # never closed by this script: the atexit teardown closes it
+    torch.zeros(1, device="cuda")
+""")
+
+
+def test_exit_teardown_after_python_threads_used_the_ring(tmp_path):
+    """the process exit after Python threads used the submission ring.  The
+    binding's atexit handler closes every open Engine, then icrc_shutdown stops the default engine's
+    ring and destroys it and frees the threads' staging slots — before the interpreter, torch and the
+    HIP runtime finalise; afterwards calls are refused before any HIP call.  The process exits 0."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, "open-rdma-driver_amd"), os.path.join(root, "oracle")]
+    script = tmp_path / "exit_probe.py"
+    script.write_text(EXIT_SCRIPT.format(paths=paths))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+    rec = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert rec["jobs"] and rec["jobs"][0] >= 600, rec
+    b, a = rec["before"], rec["after"]
+    assert b["shutdown"] == 1 and b["engines_destroyed"] >= 1 and b["slots_freed"] >= 1, rec
+    assert rec["err"] == -5 and a["refused_after"] > b["refused_after"] and rec["devices"] == 0, rec
