@@ -277,13 +277,8 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     return rc;
 }
 
-// The CUs a device batch can have: all of them, less those the engine's submission ring holds while
-// its service kernel is resident (one 160 KiB-LDS workgroup per CU, 32 by default).  Every batch
-// kernel is a persistent grid of one workgroup per CU with a fixed share per workgroup: a grid that
-// counted the ring's CUs would leave those workgroups queued until the ring's kernel ends (up to its
-// 1 ms lifetime) and the whole batch would wait for them.
-// Live rings (every engine's, with its device), never destroyed: read by device dispatch (free_cus)
-// and stopped at process exit if icrc_shutdown never ran (ring_atexit).
+// Live rings (every engine's, with its device), never destroyed: stopped at process exit if
+// icrc_shutdown never ran (ring_atexit); read by the A/B grid below.
 struct RingEntry {
     int device;
     icrc::HostRing *ring;
@@ -291,21 +286,29 @@ struct RingEntry {
 std::mutex g_ring_mu;
 std::vector<RingEntry> &g_rings = *new std::vector<RingEntry>();
 
+// (A/B, ICRC_AB_RING_AWARE=1) a device batch's grid without the CUs the engine's submission ring
+// holds while its service kernel is resident (one 160 KiB-LDS workgroup per CU, 32 by default).
+// Measured and rejected (scripts/probe_ring_c1.py): C1 with a busy
+// ring 0.78-0.80 ms on the full grid (its queued workgroups start as the ring's kernel ends, within
+// its 1 ms life) against 0.84-0.86 on the smaller grid (the ring's CUs idle once its kernel ends),
+// 0.72 alone.  The product keeps the full grid.
 int free_cus(const icrc_engine *e) {
 #ifdef ICRC_AB_BUILD
     static const bool aware = [] {
         const char *v = std::getenv("ICRC_AB_RING_AWARE");
-        return !v || std::atoi(v) != 0;
+        return v && std::atoi(v) != 0;
     }();
-    if (!aware) return e->num_cu;
-#endif
-    int held = 0;  // any engine's ring on this device (the default engine's, an Engine's of its own)
-    {
-        std::lock_guard<std::mutex> lk(g_ring_mu);
-        for (const RingEntry &r : g_rings)
-            if (r.device == e->device && r.ring->live()) held += static_cast<int>(r.ring->workgroups());
+    if (aware) {
+        int held = 0;  // any engine's ring on this device
+        {
+            std::lock_guard<std::mutex> lk(g_ring_mu);
+            for (const RingEntry &r : g_rings)
+                if (r.device == e->device && r.ring->live()) held += static_cast<int>(r.ring->workgroups());
+        }
+        return held < e->num_cu ? e->num_cu - held : e->num_cu;
     }
-    return held < e->num_cu ? e->num_cu - held : e->num_cu;
+#endif
+    return e->num_cu;
 }
 
 int grid_for(const icrc_engine *e, uint32_t n) {
