@@ -135,6 +135,8 @@ struct icrc_engine {
     std::atomic<int> host_path{ICRC_HOST_RING};  // scalar calls and host messages: the submission ring or launches
     std::mutex ring_mu;
     std::unique_ptr<struct RingState> ring;  // the submission ring (created on first use)
+    uint32_t *d_rx_flag = nullptr;          // the ragged receive's sweep flag (BatchParams::rx_flag)
+    std::atomic<uint32_t> rx_gen{0};        // ... and its per-call generation
 };
 
 namespace {
@@ -1205,6 +1207,7 @@ int engine_teardown(icrc_engine *e) {
     combiner_free(e);
     if (e->d_table) (void)hipFree(e->d_table);
     if (e->d_table_oct) (void)hipFree(e->d_table_oct);
+    if (e->d_rx_flag) (void)hipFree(e->d_rx_flag);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
@@ -1303,7 +1306,8 @@ int icrc_engine_create(int device, icrc_engine **out) {
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&e->d_rx_flag, 256) != hipSuccess || hipMemset(e->d_rx_flag, 0, 256) != hipSuccess) {
         (void)engine_teardown(e);
         delete e;
         return ICRC_EDEVICE;
@@ -1546,16 +1550,20 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
         return icrc::launch_oct_rx(p, grid_for(e, n), stream, rx_oct_knob());
     }
     // Ragged batches with whole 64-packet blocks per wave: the same one-pass receive on the packets
-    // the oct kernel takes and the long-packet verify on the rest in one launch, then descriptors
-    // for the rest from their header words (icrc_rx_sweep_kernel).  p.ok carries the long packets'
-    // results to that last step: a stream-ordered scratch array when the caller passes none.  (A/B:
-    // ICRC_AB_RX_OCT=0 keeps the two passes.)
+    // the oct kernel takes and the long-packet verify + descriptors on the rest in one launch, then
+    // (only when the ring's tail loop took any) descriptors for those from their header words
+    // (icrc_rx_sweep_kernel).  p.ok carries the tail loop's results to that last step: a
+    // stream-ordered scratch array when the caller passes none.  (A/B: ICRC_AB_RX_OCT=0 keeps the
+    // two passes.)
     {
         const int grid = grid_for(e, n);
         if (e->variant < 0 && (d_off || d_len) && rx_oct_knob() != 0 &&
             static_cast<uint64_t>(n) > 32ull * icrc::kWavesPerGroup * static_cast<uint64_t>(grid)) {
             p.table_oct = e->d_table_oct;
             p.split_len = icrc::split_len_for(icrc::kDefaultRaggedVariant);
+            uint32_t gen = e->rx_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+            p.rx_flag = e->d_rx_flag;
+            p.rx_gen = gen ? gen : 1u;  // (after a wrap the flag stays high: every call sweeps, still exact)
             uint8_t *scratch = nullptr;
             hipStream_t s = static_cast<hipStream_t>(stream);
             if (!d_ok) HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&scratch), n, s));

@@ -71,6 +71,11 @@ struct BatchParams {
     int spread;          // one-packet pipeline: consecutive waves' packets on different workgroups
                          // (small host-mapped batches: more CUs issue PCIe reads at once)
     uint32_t skew = kWaveSkew;  // persistent waves' work shares by age (wave_range, icrc_device.h)
+    // ragged one-pass receive: the sweep (icrc_rx_sweep_kernel) runs only when the ring found packets
+    // it leaves to it (its tail loop's): the ring raises *rx_flag to rx_gen (atomicMax), the sweep
+    // exits when *rx_flag < rx_gen.  rx_gen grows per call of the engine (0: no flag, always sweep).
+    uint32_t *rx_flag = nullptr;
+    uint32_t rx_gen = 0;
 };
 
 constexpr int kDefaultVariant = 16;  // S=2 chains, D=1, nt row loads (A/B: profiles/r01_ab_c1_depth.json)

@@ -499,14 +499,21 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
             }
             __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, SAUX);
             const uint32_t uu = CUT < 2 ? w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u)) : w;
-            if constexpr (CUT == 0) acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
+            if constexpr (CUT == 0 || CUT >= 3) acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
             else acc ^= uu;
         }
-        const uint32_t crc = ~wave_xor(CUT == 0 ? final_mul(lds, acc, c.fin) : acc);
+        const uint32_t crc = ~wave_xor((CUT == 0 || CUT >= 3) ? final_mul(lds, acc, c.fin) : acc);
         const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
             pbase, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
-        send_record(res, pkt_len, icrc_out, npk, g.pk, g.L - g.skip, crc, g.fast, lane);
+        if constexpr (CUT != 4)
+            __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
+        if constexpr (CUT < 3) {
+            send_record(res, pkt_len, icrc_out, npk, g.pk, g.L - g.skip, crc, g.fast, lane);
+        } else {  // (A/B 7 / 8: the per-packet result-record stores, out of range but for a block flush, cut)
+            res.block = static_cast<int>(g.pk >> 6);
+            rb_put(res.len, g.pk, g.L - g.skip);
+            rb_put(res.crc, g.pk, crc);
+        }
     };
 
     constexpr int B = D + 1;
@@ -908,9 +915,13 @@ int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
                        p.msgs, p.nmsgs, p.npackets, p.wire, p.wire_bytes, p.pkt_len, p.icrc, p.table)
 #ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK = 0 the product shape; 1: two packets in flight; 2: nt wire stores;
     // 3: nt payload loads; 4: nt loads and stores; 5: rows XOR-folded (no CRC tables); 6: 5 without
-    // the header / mask / pad selects (results wrong by design for 5 and 6)
+    // the header / mask / pad selects; 7: the full kernel without the per-packet result-record stores
+    // (all but the chunk's last block of pkt_len / icrc lost); 8: 7 without the trailer store
+    // (results wrong by design for 5-8)
     const char *v = std::getenv("ICRC_AB_PK");
     switch (v ? std::atoi(v) : 0) {
+    case 7: ICRC_PK(1, 0, 0, 3); break;
+    case 8: ICRC_PK(1, 0, 0, 4); break;
     case 5: ICRC_PK(1, 0, 0, 1); break;
     case 6: ICRC_PK(1, 0, 0, 2); break;
     case 1: ICRC_PK(2, 0, 0); break;

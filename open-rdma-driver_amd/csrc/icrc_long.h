@@ -780,7 +780,9 @@ __device__ __forceinline__ void run_pipelined(const BatchParams &p, const char *
 // Packets in flight ahead of the one being stepped (3 measured the same on C2: the long half's
 // tail is the CUs freeing up from the short-packet kernel, not the walk's latency).
 constexpr int kLongWalkDepth = 1;
-template <int MODE, int D, class A, bool TRAILER>
+// PARSE 2 (the ragged one-pass receive's long half): each long packet's descriptor collected as in
+// the fused small-batch receive (RxAcc) and stored with its block's ok bytes.
+template <int MODE, int D, class A, bool TRAILER, int PARSE = 0>
 __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const char *lds, const LaneConsts &c,
                                                    uint32_t lane, uint32_t lo, uint32_t nq) {
     constexpr int B = D + 1;
@@ -796,7 +798,8 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     int rb_block = -1;
     HeadMasks hm;
     head_masks_init(hm);
-    RxAcc ra;  // unused (no parse here)
+    RxAcc ra;  // PARSE 2: the current result block's descriptors
+    if constexpr (PARSE == 2) rx_acc_init(ra);
     SlotMeta m[B][1];
     uint32_t qs[B];
     uint32_t u[B][1][ring_words<MODE>()];
@@ -859,17 +862,23 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
             if (m[b][0].kind) {
                 const int blk = static_cast<int>(qs[b] >> 6);
                 if (blk != rb_block) {
-                    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+                    if (rb.valid) {
+                        if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + static_cast<uint32_t>(rb_block) * 64u, rb.v, lane);
+                        rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+                    }
                     rb_block = blk;
                 }
-                process_set<MODE, 1, A, 0, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
+                process_set<MODE, 1, A, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
                 inflight -= 1;
             }
             return true;
         });
         if (qn >= nq && inflight == 0) break;
     }
-    if (rb.valid) rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+    if (rb.valid) {
+        if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + static_cast<uint32_t>(rb_block) * 64u, rb.v, lane);
+        rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+    }
 }
 
 // Default (COMPACT = false): per wave, the C1 pipeline (S = 2 chains, D = 1) over the wave's whole
@@ -902,7 +911,8 @@ __device__ __forceinline__ bool wg_any_split(const BatchParams &p, uint4 *lds4, 
 
 // The long-packet kernel's work for workgroup `bid` of `nblk` (its own kernel, or the long-packet
 // workgroups of the fused hybrid kernel, icrc_oct.hip).
-template <int MODE, bool COMPACT, bool TRAILER, class LA = Ring<kStreamAux>>
+// PARSE 2: the ragged one-pass receive's long half (descriptors of the long packets, RxAcc).
+template <int MODE, bool COMPACT, bool TRAILER, class LA = Ring<kStreamAux>, int PARSE = 0>
 __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uint32_t bid, uint32_t nblk) {
     if (p.split_len != 0 && p.len != nullptr) {
         // A workgroup whose packets are all the oct kernel's exits before its 160 KiB table load.
@@ -941,7 +951,7 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
     const uint32_t lo = static_cast<uint32_t>(lo64);
     const uint32_t nq = static_cast<uint32_t>((hi64 < p.n ? hi64 : p.n) - lo64);
     if constexpr (COMPACT) {
-        run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER>(p, lds, c, lane, lo, nq);
+        run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);
     } else {
         // Per wave, by the density of long packets in its first 64-packet block: dense (>= 3/4,
         // e.g. a 4 KiB WRITE stream) -> the C1 pipeline with short packets as empty slots; sparse
@@ -950,9 +960,9 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, LA, 0, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
+            run_pipelined<MODE, 2, 1, LA, PARSE, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
         else
-            run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER>(p, lds, c, lane, lo, nq);
+            run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);
     }
 }
 

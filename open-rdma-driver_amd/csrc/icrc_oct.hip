@@ -912,6 +912,8 @@ __device__ __forceinline__ void run_oct(const BatchParams &p, const char *lds, c
     }
     if (nres) flush();
     if (RX && rx_pend) rx_readback(rx_pbase, rx_pcnt);
+    // (ragged receive) packets left to the tail loop below: their descriptors are the sweep's
+    if (RX && RAGGED && irregular && p.rx_flag && lane == 0) atomicMax(p.rx_flag, p.rx_gen);
     if (bailed) {  // never reached by correct bookkeeping: make it loud, not silent
         for (uint32_t i = lane; i < nq; i += 64u) store_result<MODE>(p, lo + i, MODE == kCompute ? 0u : ICRC_VERIFY_BADLEN);
         if (p.nerr && lane == 0) atomicAdd(p.nerr, nq);
@@ -1069,18 +1071,22 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_rx_kernel(BatchP
     uint32_t lo, nq;
     rx_oct_part<TRAILER, OctProduct, true>(p, lds4, lo, nq);
     __syncthreads();  // every wave is done with the receive image before the long body rewrites LDS
-    long_body<kVerify, false, TRAILER>(p, lds4, blockIdx.x, gridDim.x);
+    long_body<kVerify, false, TRAILER, Ring<kStreamAux>, 2>(p, lds4, blockIdx.x, gridDim.x);  // + their descriptors
 }
 
-// Launch 2: descriptors for every packet the ring did not take (L >= split_len, verified by
-// long_body; L < 44, misaligned, far apart: the ring's tail loop), from their header words and the
-// ok bytes those paths left in p.ok, in the descriptor pass's shape (rx_desc_block).  The ring's
+// Launch 2: descriptors for the short packets the ring did not take (L < 44, misaligned, far apart:
+// the ring's tail loop), from their header words and the ok bytes the tail loop left in p.ok, in the
+// descriptor pass's shape (rx_desc_block); a call whose ring left none (p.rx_flag below p.rx_gen)
+// returns at once.  The long packets' descriptors are long_body's (PARSE 2, round 6: on configs[2]
+// this launch took 69 us for them, 12 % of the receive).  The ring's
 // blocks are whole, 64-aligned blocks of the batch (the dispatch guarantees more than 32 packets
 // per wave), so classifying each block here again (oct_block) finds exactly the ring's packets.
 // (In the first launch, after long_body, this measured slower: that kernel's registers are sized
 // for its rings.)
 __global__ __launch_bounds__(256) void icrc_rx_sweep_kernel(BatchParams p) {
     __shared__ uint32_t sh_all[4 * 64 * kRxStride];
+    // nothing left by the ring's tail loop in this call (the long packets' descriptors are long_body's)
+    if (p.rx_flag && *reinterpret_cast<volatile const uint32_t *>(p.rx_flag) < p.rx_gen) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *sh = sh_all + wave * 64u * kRxStride;
@@ -1092,7 +1098,7 @@ __global__ __launch_bounds__(256) void icrc_rx_sweep_kernel(BatchParams p) {
         const uint32_t L = valid ? (p.len ? p.len[i] : p.ulen) : 0u;
         OctBlock B;
         oct_block<kVerify>(p, B, off, L, valid, base, 0, lane);
-        const uint64_t need = __ballot(valid) & ~B.mine;
+        const uint64_t need = __ballot(valid && L < p.split_len) & ~B.mine;
         if (need != 0ull) rx_desc_block(p, sh, base, p.n - base < 64u ? p.n - base : 64u, need, lane);
     }
 }

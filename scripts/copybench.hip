@@ -25,7 +25,12 @@ constexpr uint32_t kPay = 4096, kWire = 4156, kN = 786432, kHdr = 56;
 
 // one wave per packet, contiguous chunks, the next packet's rows loaded while the current one is
 // stored (a two-slot register ring)
-template <int POLICY_ST, bool IL = false>
+// LSHIFT: the payload loads start LSHIFT bytes before each 256-B source row (the packetizer's end-
+// aligned rows put its loads 4 (k0 - 1 - hw) = -252 mod 256 bytes off the payload's lines, so every
+// 256-B row load touches 5 lines instead of 4); the bytes outside the payload read as 0 (range check)
+// WIRE / HDR: the wire slot stride and the payload's offset in it (4156 / 56: the packetizer's
+// packets; 4160 / 0 with LSHIFT 56: every row store line-aligned, every row load 56 B off its lines)
+template <int POLICY_ST, bool IL = false, int LSHIFT = 0, uint32_t WIRE = kWire, uint32_t HDR = kHdr>
 __global__ __launch_bounds__(1024) void rows_dword(const uint8_t *src, uint8_t *dst, uint32_t waves) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -41,13 +46,16 @@ __global__ __launch_bounds__(1024) void rows_dword(const uint8_t *src, uint8_t *
     auto load = [&](uint32_t q, uint32_t (&u)[R]) {
         auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + pkt(q) * kPay), 0, (int)kPay, 0x00020000);
 #pragma unroll
-        for (int j = 0; j < R; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * lane + 256u * j), 0, 0);
+        for (int j = 0; j < R; ++j) {
+            const int o = (int)(4u * lane + 256u * j) - LSHIFT;
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, o >= 0 ? o : (int)0x80000000, 0, 0);
+        }
     };
     auto store = [&](uint32_t q, uint32_t (&u)[R]) {
-        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + pkt(q) * kWire), 0, (int)kWire, 0x00020000);
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + pkt(q) * WIRE), 0, (int)WIRE, 0x00020000);
 #pragma unroll
         for (int j = 0; j < R; ++j)
-            __builtin_amdgcn_raw_buffer_store_b32(u[j], rs, (int)(kHdr + 4u * lane + 256u * j), 0, POLICY_ST);
+            __builtin_amdgcn_raw_buffer_store_b32(u[j], rs, (int)(HDR + 4u * lane + 256u * j) - (HDR == 0 ? 0 : LSHIFT), 0, POLICY_ST);
     };
     load(0, ua);
     for (uint32_t q = 0; q < nq; q += 2) {
@@ -160,7 +168,7 @@ int main() {
     uint8_t *src, *dst;
     const size_t src_bytes = (size_t)1048576 * 4156 + 4096;  // >= kN * kPay; the C1 read shape reads 1 Mi x 4156 B
     CK(hipMalloc(&src, src_bytes));
-    CK(hipMalloc(&dst, (size_t)kN * kWire + 4096));
+    CK(hipMalloc(&dst, (size_t)kN * 4160 + 4096));
     CK(hipMemset(src, 0x5a, src_bytes));
     const bool rnd = getenv("COPY_RAND") && atoi(getenv("COPY_RAND")) == 1;
     if (rnd) {
@@ -196,6 +204,23 @@ int main() {
             report(nm, time_it([&] { rows_x4<0, true><<<grid, 1024>>>(src, dst, waves); }, reps));
             snprintf(nm, sizeof nm, "rows_x4 %d waves/CU, interleaved packets, nt stores", w);
             report(nm, time_it([&] { rows_x4<2, true><<<grid, 1024>>>(src, dst, waves); }, reps));
+        }
+        if (getenv("COPY_SHIFT")) {  // the packetizer's load misalignment against the aligned rows
+            const uint32_t waves = cus * 16;
+            report("rows_dword 16 waves/CU (aligned loads)", time_it([&] { rows_dword<0><<<cus, 1024>>>(src, dst, waves); }, reps));
+            report("rows_dword 16 waves/CU, loads 252 B before each row (packetizer shape)",
+                   time_it([&] { rows_dword<0, false, 252><<<cus, 1024>>>(src, dst, waves); }, reps));
+            report("rows_dword 16 waves/CU, loads 64 B before each row (line aligned)",
+                   time_it([&] { rows_dword<0, false, 64><<<cus, 1024>>>(src, dst, waves); }, reps));
+            report("rows_dword 16 waves/CU, loads 4 B before each row",
+                   time_it([&] { rows_dword<0, false, 4><<<cus, 1024>>>(src, dst, waves); }, reps));
+            report("rows_dword 16 waves/CU, slots of 4160 B: stores line-aligned, loads 56 B off",
+                   time_it([&] { rows_dword<0, false, 56, 4160, 0><<<cus, 1024>>>(src, dst, waves); }, reps));
+            report("rows_dword 16 waves/CU, slots of 4160 B: stores and loads line-aligned",
+                   time_it([&] { rows_dword<0, false, 0, 4160, 0><<<cus, 1024>>>(src, dst, waves); }, reps));
+            const size_t n16 = (size_t)kN * kPay / 16;
+            report("flat_x4 contiguous 16 waves/CU", time_it([&] { flat_x4<<<cus * 4, 256>>>((const uint4 *)src, (uint4 *)dst, n16); }, reps));
+            continue;
         }
         for (int w : {16, 32}) {
             const uint32_t waves = cus * w;

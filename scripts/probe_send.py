@@ -8,7 +8,8 @@ packet 128-byte aligned) and 8192 (the reference's own per-packet buffer, net/ut
 algorithmic bytes per packet (4096 read + 4156 written + 8) are the same for every stride.  After
 the packetizer, a device-to-device copy of the payload bytes (hipMemcpyAsync) is timed beside it.
 
-usage: probe_send.py [reps] [variant ...] [--strides 4156,4224,8192]   (-1 = the default dispatch)"""
+usage: probe_send.py [reps] [variant ...] [--strides 4156,4224,8192]   (-1 = the default dispatch;
+pkN = the default dispatch with ICRC_AB_PK=N, the A/B library's packetizer shapes and cuts)"""
 import json
 import os
 import sys
@@ -47,15 +48,16 @@ def main():
     ic = torch.zeros(npk, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
     builds = []
-    for v in [int(x) for x in args[1:]] or [-1]:
+    for x in args[1:] or ["-1"]:
         eng = icrc_amd.Engine(0, lib=icrc_amd.ab_library())  # A/B library: diagnostic variants
-        eng.set_variant(v)
-        builds.append((v, eng))
+        eng.set_variant(-1 if x.startswith("pk") else int(x))
+        builds.append((x, eng))
     alg = npk * (4096 + 4156 + 8)
     ref = {}
     for r in range(reps):
         for (name, eng), st in [(b, st) for b in builds for st in strides]:
             dm = per_stride[st]
+            os.environ["ICRC_AB_PK"] = name[2:] if str(name).startswith("pk") else "0"  # read per launch
 
             def launch():
                 eng.packetize(src.data_ptr(), src.numel(), dm.data_ptr(), nmsg, npk, wire.data_ptr(), npk * st,
@@ -73,7 +75,8 @@ def main():
                 ms.append(a.elapsed_time(b) / 10)
             med = float(np.median(ms))
             h = (int(ic.sum().item()), int(ln.sum().item()))  # ICRCs and lengths: the same at every stride
-            ref.setdefault("h", h)
+            if str(name) in ("-1", "pk0"):
+                ref.setdefault("h", h)
             print(json.dumps({"variant": name, "slot_stride": st, "rep": r, "ms_median": round(med, 4),
                               "ms_min": round(min(ms), 4), "GB/s (read+write)": round(alg / (med * 1e-3) / 1e9, 1),
                               "frac_of_8TB/s": round(alg / (med * 1e-3) / 8e12, 4), "same_output": h == ref["h"]}),
