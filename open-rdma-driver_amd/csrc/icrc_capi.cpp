@@ -192,6 +192,7 @@ struct DispatchKnobs {
     int long_cus = 0;            // ICRC_AB_LONG_CUS: CUs running long-packet workgroups from the start
     int long_self = 1;           // ICRC_AB_LONG_SELF=0: the two workgroup sets (oct, then long-packet ones)
     int self_grid_mult = 1;      // ICRC_AB_SELF_GRID: workgroups per CU of the in-place hybrid (smaller ranges)
+    int long_walk = 0;           // ICRC_AB_LONG_WALK=1: run_walk_masked (icrc_long.h; measured, rejected)
 };
 DispatchKnobs dispatch_knobs() {
     DispatchKnobs k;
@@ -210,6 +211,7 @@ DispatchKnobs dispatch_knobs() {
     k.long_cus = env("ICRC_AB_LONG_CUS", 0);
     k.long_self = env("ICRC_AB_LONG_SELF", 1);
     k.self_grid_mult = std::max(1, std::min(8, env("ICRC_AB_SELF_GRID", 1)));
+    k.long_walk = env("ICRC_AB_LONG_WALK", 0);
 #endif
     return k;
 }
@@ -230,6 +232,7 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
                                                                     static_cast<uint32_t>(e->num_cu)))
                               : grid_for(e, p.n);
     p.split_len = 0;
+    p.ab_long_walk = static_cast<uint32_t>(k.long_walk);
     if (k.skew >= 0) p.skew = static_cast<uint32_t>(k.skew) * 0x10001u;
     if (k.skew_oct >= 0) p.skew = (p.skew & 0xFFFF0000u) | (static_cast<uint32_t>(k.skew_oct) & 0xFFFFu);
     if (k.skew_long >= 0) p.skew = (p.skew & 0xFFFFu) | (static_cast<uint32_t>(k.skew_long) << 16);
@@ -1561,6 +1564,7 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
             static_cast<uint64_t>(n) > 32ull * icrc::kWavesPerGroup * static_cast<uint64_t>(grid)) {
             p.table_oct = e->d_table_oct;
             p.split_len = icrc::split_len_for(icrc::kDefaultRaggedVariant);
+            p.ab_long_walk = static_cast<uint32_t>(dispatch_knobs().long_walk);
             uint32_t gen = e->rx_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
             p.rx_flag = e->d_rx_flag;
             p.rx_gen = gen ? gen : 1u;  // (after a wrap the flag stays high: every call sweeps, still exact)

@@ -368,6 +368,8 @@ struct SendResults {
     int block;
 };
 
+// COND (A/B 9): the two stores under a (uniform) branch, issued only when a block leaves.
+template <bool COND = false>
 __device__ __forceinline__ void send_record(SendResults &r, uint32_t *pkt_len, uint32_t *icrc_out, uint32_t npk,
                                             uint32_t pk, uint32_t L, uint32_t crc, bool valid, uint32_t lane) {
     const int blk = static_cast<int>(pk >> 6);
@@ -376,8 +378,10 @@ __device__ __forceinline__ void send_record(SendResults &r, uint32_t *pkt_len, u
     const bool mine = flush && ((r.len.valid >> lane) & 1ull);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(pkt_len, 0, pkt_len ? static_cast<int>(npk * 4u) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(icrc_out, 0, icrc_out ? static_cast<int>(npk * 4u) : 0, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(r.len.v, rl, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(r.crc.v, rc, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
+    if (!COND || flush) {
+        __builtin_amdgcn_raw_buffer_store_b32(r.len.v, rl, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(r.crc.v, rc, static_cast<int>(mine ? 4u * idx : kSendOOR), 0, 0);
+    }
     if (flush) r.len.valid = r.crc.valid = 0;
     if (valid) {
         r.block = blk;
@@ -492,23 +496,23 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_packetize_kernel(const 
         for (int j = 0; j < kRows; ++j) {
             const int pw = g.k0 - 1 + static_cast<int>(lane) + 64 * j;
             uint32_t w = u[j];
-            if constexpr (CUT < 2) w = (j == jh && inA) ? hA : ((j == jh + 1 && inB) ? hB : w);
-            if (CUT < 2 && j == kRows - 1) {  // the packet's last word: payload bytes only, then the zero pad
+            if constexpr (CUT != 2) w = (j == jh && inA) ? hA : ((j == jh + 1 && inB) ? hB : w);
+            if (CUT != 2 && j == kRows - 1) {  // the packet's last word: payload bytes only, then the zero pad
                 const int keep = static_cast<int>(room) - 4 * pw;
                 w = keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
             }
             __builtin_amdgcn_raw_buffer_store_b32(w, os, pw >= pw_lo ? 4 * pw : static_cast<int>(kSendOOR), 0, SAUX);
-            const uint32_t uu = CUT < 2 ? w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u)) : w;
+            const uint32_t uu = CUT != 2 ? w | (j == j0 ? mA : (j == j0 + 1 ? mB : 0u)) : w;
             if constexpr (CUT == 0 || CUT >= 3) acc = j == 0 ? uu : step_m64(lds, acc, uu, c);
             else acc ^= uu;
         }
-        const uint32_t crc = ~wave_xor((CUT == 0 || CUT >= 3) ? final_mul(lds, acc, c.fin) : acc);
+        const uint32_t crc = ~wave_xor((CUT == 0 || CUT >= 3) ? final_mul(lds, acc, c.fin) : acc);  // (CUT 5: exact)
         const __amdgpu_buffer_rsrc_t ts = __builtin_amdgcn_make_buffer_rsrc(
             pbase, 0, g.fast ? static_cast<int>(g.L) : 0, 0x00020000);
         if constexpr (CUT != 4)
             __builtin_amdgcn_raw_buffer_store_b32(crc, ts, static_cast<int>(lane == 0 ? g.L - 4u : kSendOOR), 0, 0);
-        if constexpr (CUT < 3) {
-            send_record(res, pkt_len, icrc_out, npk, g.pk, g.L - g.skip, crc, g.fast, lane);
+        if constexpr (CUT < 3 || CUT == 5) {
+            send_record<CUT == 5>(res, pkt_len, icrc_out, npk, g.pk, g.L - g.skip, crc, g.fast, lane);
         } else {  // (A/B 7 / 8: the per-packet result-record stores, out of range but for a block flush, cut)
             res.block = static_cast<int>(g.pk >> 6);
             rb_put(res.len, g.pk, g.L - g.skip);
@@ -736,9 +740,11 @@ __global__ __launch_bounds__(256) void icrc_synth_kernel(uint8_t *base, const ic
 // A/B: the fixed cost of a small-batch launch (configs[3]: 4096 packets, one per wave), decomposed
 // (VERDICT r05 item 2).  Same grid, block and LDS size as icrc_batch_kernel; each wave stores one
 // result per packet of its one-packet range (as the batch kernel's final store) and nothing else:
-//   CUT 0 (variant 24) the launch alone (waves start, the LDS image is allocated, one store);
-//   CUT 1 (25) + the table image into LDS (table_fetch / table_store, the barrier);
-//   CUT 2 (26) + each wave's (offset, length) load before the table wait (a ragged batch's meta).
+//   CUT 0 (variant 27) the launch alone (waves start, the LDS image is allocated, one store);
+//   CUT 1 (28) + the table image into LDS (table_fetch / table_store, the barrier);
+//   CUT 2 (29) + each wave's (offset, length) load before the table wait (a ragged batch's meta).
+// (Numbered 24-26 in the first record, profiles/r06/c3/: those numbers belong to the retired quad
+// kernels, which both libraries refuse.)
 template <int MODE, int CUT>
 __global__ __launch_bounds__(kThreadsPerGroup) void icrc_fixed_cost_kernel(BatchParams p) {
     __shared__ uint4 lds4[kLdsBytes / 16];
@@ -800,9 +806,9 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 21: ICRC_LAUNCH(2, 1, RingNoFinal, false); break;   // 16 without final products
     case 22: ICRC_LAUNCH(2, 1, RingNoStore, false); break;   // 16 without result stores
     case 23: ICRC_LAUNCH(2, 1, RingBare, false); break;      // 19 without final products and stores
-    case 24: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 0>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-    case 25: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
-    case 26: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 27: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 0>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 28: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 29: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products
@@ -916,12 +922,13 @@ int launch_packetize(const PacketizeParams &p, int grid, void *stream) {
 #ifdef ICRC_AB_BUILD  // A/B: ICRC_AB_PK = 0 the product shape; 1: two packets in flight; 2: nt wire stores;
     // 3: nt payload loads; 4: nt loads and stores; 5: rows XOR-folded (no CRC tables); 6: 5 without
     // the header / mask / pad selects; 7: the full kernel without the per-packet result-record stores
-    // (all but the chunk's last block of pkt_len / icrc lost); 8: 7 without the trailer store
-    // (results wrong by design for 5-8)
+    // (all but the chunk's last block of pkt_len / icrc lost); 8: 7 without the trailer store; 9: the
+    // record stores under a branch, only when a block leaves (exact) (results wrong by design for 5-8)
     const char *v = std::getenv("ICRC_AB_PK");
     switch (v ? std::atoi(v) : 0) {
     case 7: ICRC_PK(1, 0, 0, 3); break;
     case 8: ICRC_PK(1, 0, 0, 4); break;
+    case 9: ICRC_PK(1, 0, 0, 5); break;
     case 5: ICRC_PK(1, 0, 0, 1); break;
     case 6: ICRC_PK(1, 0, 0, 2); break;
     case 1: ICRC_PK(2, 0, 0); break;

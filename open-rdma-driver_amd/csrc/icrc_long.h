@@ -881,6 +881,162 @@ __device__ __forceinline__ void run_pipelined_long(const BatchParams &p, const c
     }
 }
 
+// A sparse long-packet walk tried in round 6 (A/B only, see long_walk_masked below).
+// run_pipelined_long above fetches each 64-packet block's
+// (offset, length) when its walk reaches the block and waits for it there, so every block costs a
+// memory round trip with the ring drained (a conditional load: vmcnt(0)); on configs[2] (1.4 % long
+// packets) that is about one round trip per long packet.  Here the wave scans its range for long
+// packets 1024 at a time (16 vector loads of 64 lengths issued together, one wait; lane j of two
+// VGPRs = the long-packet mask of block j of the group), and each long packet's (offset, length)
+// comes by a vector load issued one packet ahead, before that packet's row loads, every step
+// (out of range when there is none), so no wait in the ring is for more than the loads already
+// behind it.
+template <int MODE, class A, bool TRAILER, int PARSE = 0>
+__device__ __forceinline__ void run_walk_masked(const BatchParams &p, const char *lds, const LaneConsts &c,
+                                                uint32_t lane, uint32_t lo, uint32_t nq) {
+    constexpr int B = 2;  // one packet's rows in flight while the previous one is stepped
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    if (nq == 0) return;
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(p.len ? p.len + lo : nullptr), 0, p.len ? static_cast<int>(nq * 4u) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t *>(p.off ? p.off + lo : nullptr), 0, p.off ? static_cast<int>(nq * 8u) : 0, 0x00020000);
+    uint32_t gm_lo = 0, gm_hi = 0;  // lane j < 16: the long packets of block 16 grp + j
+    int grp = -1;
+    uint32_t qn = 0;  // next candidate
+    auto find = [&]() __attribute__((always_inline)) -> uint32_t {
+        while (qn < nq) {
+            const uint32_t blk = qn >> 6, g = blk >> 4;
+            if (static_cast<int>(g) != grp) {  // a new group of 16 blocks: one round trip for all of them
+                uint32_t lv[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    lv[j] = p.len ? __builtin_amdgcn_raw_buffer_load_b32(rl, static_cast<int>(((g * 16u + j) * 64u + lane) * 4u), 0, 0)
+                                  : ((g * 16u + j) * 64u + lane < nq ? p.ulen : 0u);
+                uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t m = __ballot(lv[j] >= p.split_len);
+                    mlo = lane == static_cast<uint32_t>(j) ? static_cast<uint32_t>(m) : mlo;
+                    mhi = lane == static_cast<uint32_t>(j) ? static_cast<uint32_t>(m >> 32) : mhi;
+                }
+                gm_lo = mlo;
+                gm_hi = mhi;
+                grp = static_cast<int>(g);
+            }
+            const int j = static_cast<int>(blk & 15u);
+            const uint64_t m = ((static_cast<uint64_t>(readlane_u32(gm_hi, j)) << 32) | readlane_u32(gm_lo, j)) &
+                               (~0ull << (qn & 63u));
+            if (m == 0ull) {
+                qn = (blk + 1u) * 64u;
+                continue;
+            }
+            const uint32_t q = blk * 64u + static_cast<uint32_t>(__builtin_ctzll(m));
+            qn = q + 1u;
+            return q;
+        }
+        return kNone;
+    };
+    // the pending packet: its index and (lane 0) its (offset, length), loaded one packet ahead
+    uint32_t pq = find();
+    uint32_t pv_lo = 0, pv_hi = 0, pv_len = 0;
+    auto pload = [&]() __attribute__((always_inline)) {  // unconditional: out of range when there is none
+        const bool have = pq != kNone && lane == 0u;
+        const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, have ? static_cast<int>(pq * 8u) : static_cast<int>(0x80000000u), 0, 0);
+        pv_lo = o[0];
+        pv_hi = o[1];
+        pv_len = __builtin_amdgcn_raw_buffer_load_b32(rl, have ? static_cast<int>(pq * 4u) : static_cast<int>(0x80000000u), 0, 0);
+    };
+    pload();
+    auto next = [&](SlotMeta &sm, uint32_t &q) __attribute__((always_inline)) {
+        sm.kind = 0;
+        sm.R = 0;
+        sm.k0 = 0;
+        sm.pkt = p.base;
+        sm.L = 0;
+        q = pq;
+        if (pq == kNone) {
+            pload();  // (the same loads every step)
+            return;
+        }
+        const uint64_t off = p.off ? ((static_cast<uint64_t>(readlane_u32(pv_hi, 0)) << 32) | readlane_u32(pv_lo, 0))
+                                   : static_cast<uint64_t>(lo + pq) * p.stride;
+        const uint32_t L = p.len ? readlane_u32(pv_len, 0) : p.ulen;
+        pq = find();
+        pload();
+        sm.pkt = p.base + off;
+        sm.L = L;
+        sm.kind = 2;
+        if (((reinterpret_cast<uintptr_t>(sm.pkt) | static_cast<uintptr_t>(L)) & 3u) == 0) {
+            const int N = static_cast<int>(stream_words<MODE>(L));
+            const int R = (N + 63) >> 6;
+            if (R <= kRows) {
+                sm.kind = 1;
+                sm.R = R;
+                sm.k0 = N - 64 * R;
+            }
+        }
+    };
+
+    ResultBuf rb;
+    rb.v = 0;
+    rb.valid = 0;
+    int rb_block = -1;
+    HeadMasks hm;
+    head_masks_init(hm);
+    RxAcc ra;
+    if constexpr (PARSE == 2) rx_acc_init(ra);
+    SlotMeta m[B][1];
+    uint32_t qs[B];
+    uint32_t u[B][1][ring_words<MODE>()];
+    int inflight = 0;
+    next(m[0][0], qs[0]);
+    slot_load<A, MODE, TRAILER>(m[0][0], lane, u[0][0]);
+    if (m[0][0].kind) inflight += 1;
+    for (;;) {
+        static_for<B>([&](auto bc) __attribute__((always_inline)) -> bool {
+            constexpr int b = decltype(bc)::value;
+            constexpr int bp = (b + 1) % B;
+            next(m[bp][0], qs[bp]);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(3);
+            slot_load<A, MODE, TRAILER>(m[bp][0], lane, u[bp][0]);
+            if constexpr (A::kPrio) __builtin_amdgcn_s_setprio(0);
+            if (m[bp][0].kind) inflight += 1;
+            if (m[b][0].kind) {
+                const int blk = static_cast<int>(qs[b] >> 6);
+                if (blk != rb_block) {
+                    if (rb.valid) {
+                        if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + static_cast<uint32_t>(rb_block) * 64u, rb.v, lane);
+                        rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+                    }
+                    rb_block = blk;
+                }
+                process_set<MODE, 1, A, PARSE, TRAILER>(p, lds, c, lane, m[b], u[b], qs[b], rb, hm, ra, lo);
+                inflight -= 1;
+            }
+            return true;
+        });
+        if (pq == kNone && inflight == 0) break;
+    }
+    if (rb.valid) {
+        if constexpr (PARSE == 2) rx_acc_flush(p, ra, lo + static_cast<uint32_t>(rb_block) * 64u, rb.v, lane);
+        rb_flush<MODE>(p, rb, lo + static_cast<uint32_t>(rb_block) * 64u, lane);
+    }
+}
+
+// (A/B only, ICRC_AB_LONG_WALK=1) run_walk_masked instead of run_pipelined_long.  Measured and
+// rejected: configs[2] compute 0.428-0.436 ms against 0.425-0.430, receive 0.515-0.525 against
+// 0.511, identical results (scripts/probe_long_walk.py, profiles/r06/c2/long_walk_ab.jsonl): the
+// walk's meta round trips were not what the long half waits for.
+__device__ __forceinline__ bool long_walk_masked(const BatchParams &p) {
+#ifdef ICRC_AB_BUILD
+    return p.ab_long_walk != 0;
+#else
+    (void)p;
+    return false;
+#endif
+}
+
 // Default (COMPACT = false): per wave, the C1 pipeline (S = 2 chains, D = 1) over the wave's whole
 // chunk with short packets left as empty slots when long packets are dense — on an all-long ragged
 // batch it runs at the strided rate (1 Mi x 4156 B: 0.75 ms split vs 0.80-0.87 with the walker) —
@@ -961,6 +1117,8 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint32_t nb = nq < 64u ? nq : 64u;
         if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
             run_pipelined<MODE, 2, 1, LA, PARSE, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
+        else if (long_walk_masked(p))
+            run_walk_masked<MODE, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);
         else
             run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);
     }
