@@ -477,25 +477,33 @@ def config_c3(eng, stream, args, world, orc):
         eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), True, 0, stream)
 
     _, kms = time_kernel(rt, min(args.steps, 20), min(args.warmup, 5), world)
-    # Each kernel's own GPU time: behind a spin kernel (torch.cuda._sleep) the host has queued the
-    # events and both launches before the GPU reaches them, so the event pairs hold no host launch
-    # cost (the round trip above does: ~9 us per launch from Python).
-    per = {"compute": [], "verify": []}
-    for _ in range(max(5, min(args.steps, 20))):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        torch.cuda._sleep(2_000_000)
-        ev[0].record()
-        eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_out.data_ptr(), True, 0, stream)
-        ev[1].record()
-        eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), True, 0, stream)
-        ev[2].record()
-        ev[2].synchronize()
-        per["compute"].append(ev[0].elapsed_time(ev[1]) * 1e3)
-        per["verify"].append(ev[1].elapsed_time(ev[2]) * 1e3)
+    # Each direction's GPU time per launch: 16 launches of one kind queued behind a spin kernel
+    # (torch.cuda._sleep), so the host has enqueued all of them before the GPU reaches the first and
+    # the events see the GPU's own rate (dispatch and the gaps between kernels included, the host's
+    # ~9 us per launch from Python not).
+    def gpu_rate(fn, k=16, reps=5):
+        out = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(4_000_000)
+            e0.record()
+            for _ in range(k):
+                fn()
+            e1.record()
+            e1.synchronize()
+            out.append(e0.elapsed_time(e1) * 1e3 / k)
+        return float(np.median(out))
+
+    k_us = {"compute": gpu_rate(lambda: eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n,
+                                                         d_out.data_ptr(), True, 0, stream)),
+            "verify": gpu_rate(lambda: eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n,
+                                                        d_ok.data_ptr(), True, 0, stream))}
+    eng.compute_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_out.data_ptr(), True, 0, stream)
+    eng.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), w3.n, d_ok.data_ptr(), True, 0, stream)
+    torch.cuda.synchronize()
     fails = int(np.count_nonzero(d_out.cpu().numpy().view(np.uint32) != want))
     all_ok = bool((d_ok == 1).all().item())
     tot3 = int(w3.lens.astype(np.uint64).sum())
-    k_us = {k: float(np.median(v)) for k, v in per.items()}
     leg = {"workload": "configs[3]: 16 MiB RDMA WRITE at PMTU 4096 (4096 packets), compute + write_trailer then "
                        "verify + zero_trailer",
            "packets": w3.n, "ms_per_roundtrip": round(kms, 4),
@@ -503,11 +511,13 @@ def config_c3(eng, stream, args, world, orc):
            "frac": round(2 * tot3 / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "frac_note": "per direction: packet bytes / (round trip / 2) / 8 TB/s (HIP events over back-to-back "
                         "launches: the two kernels and the gaps between them)",
-           "kernel_us": {"compute_write_trailer": round(k_us["compute"], 2), "verify_zero_trailer": round(k_us["verify"], 2)},
-           "kernel_frac": {k: round(tot3 / (v * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) for k, v in
-                           (("compute_write_trailer", k_us["compute"]), ("verify_zero_trailer", k_us["verify"]))},
-           "kernel_note": "each kernel's GPU time (median), events queued behind a spin kernel; the launch's own "
-                          "fixed cost is in it (DESIGN §6: ~2.5 us of an empty kernel of this grid)",
+           "gpu_us_per_launch": {"compute_write_trailer": round(k_us["compute"], 2),
+                                 "verify_zero_trailer": round(k_us["verify"], 2)},
+           "gpu_frac": {k: round(tot3 / (v * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) for k, v in
+                        (("compute_write_trailer", k_us["compute"]), ("verify_zero_trailer", k_us["verify"]))},
+           "gpu_note": "16 launches of one direction queued behind a spin kernel, events around them: the GPU's "
+                       "own rate per launch (dispatch and inter-kernel gaps in it, host launch cost not); DESIGN "
+                       "§6 decomposes it (an empty kernel of this grid: ~2.5 us)",
            "all_ok": all_ok, "parity_checked": w3.n, "parity_failures": fails}
     del d_buf, d_off, d_len, d_out, d_ok
     return leg, fails + (0 if all_ok else 1)
@@ -581,8 +591,8 @@ def check_sample(orc, d_buf, d_out, n: int, L: int, k: int, rank: int, inject_ra
     return fails, checked
 
 
-PMC_TRAFFIC_FILE = "r05_pmc_traffic.json"
-PMC_C2_FILE = "r05_pmc_c2_traffic.json"
+PMC_TRAFFIC_FILE = "r06_pmc_traffic.json"
+PMC_C2_FILE = "r06_pmc_c2_traffic.json"
 # the sources the C1 kernel is built from: a traffic summary taken on another build is not this one's
 KERNEL_SOURCES = ("icrc_kernels.hip", "icrc_device.h", "icrc_long.h", "icrc_internal.h", "icrc_tables.cpp")
 # ... and the configs[2] kernel (the hybrid launch: oct + long-packet workgroups)

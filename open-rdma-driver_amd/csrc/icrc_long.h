@@ -1115,9 +1115,13 @@ __device__ __forceinline__ void long_body(const BatchParams &p, uint4 *lds4, uin
         const uint32_t L0 = lane < nq ? (p.len ? p.len[lo + lane] : p.ulen) : 0u;
         const uint64_t lm = __ballot(lane < nq && L0 >= p.split_len);
         const uint32_t nb = nq < 64u ? nq : 64u;
-        if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb)
-            run_pipelined<MODE, 2, 1, LA, PARSE, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
-        else if (long_walk_masked(p))
+        if (4u * static_cast<uint32_t>(__builtin_popcountll(lm)) >= 3u * nb) {
+            // (PARSE: a dense range's descriptors are the sweep's -- stored inside this ring they cost
+            // 786 K x 4156 B 0.608 ms against 0.540, the fused pass's old finding -- so the wave only
+            // raises the call's second sweep flag, and the sweep takes every long packet)
+            run_pipelined<MODE, 2, 1, LA, 0, true, TRAILER, false, LA::kScalarMeta>(p, lds, c, lane, lo, nq);
+            if (PARSE && p.rx_flag && lane == 0) atomicMax(p.rx_flag + 1, p.rx_gen);
+        } else if (long_walk_masked(p))
             run_walk_masked<MODE, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);
         else
             run_pipelined_long<MODE, kLongWalkDepth, Ring<kStreamAux>, TRAILER, PARSE>(p, lds, c, lane, lo, nq);

@@ -1075,18 +1075,26 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_hybrid_rx_kernel(BatchP
 }
 
 // Launch 2: descriptors for the short packets the ring did not take (L < 44, misaligned, far apart:
-// the ring's tail loop), from their header words and the ok bytes the tail loop left in p.ok, in the
-// descriptor pass's shape (rx_desc_block); a call whose ring left none (p.rx_flag below p.rx_gen)
-// returns at once.  The long packets' descriptors are long_body's (PARSE 2, round 6: on configs[2]
-// this launch took 69 us for them, 12 % of the receive).  The ring's
+// the ring's tail loop) and for the long packets of dense ranges, from their header words and the
+// ok bytes those paths left in p.ok, in the descriptor pass's shape (rx_desc_block); a call with
+// neither (p.rx_flag[0..1] below p.rx_gen) returns at once.  The long packets of sparse ranges
+// have their descriptors from long_body's walk (PARSE 2, round 6: on configs[2] this launch took
+// 69 us for them, 12 % of the receive).  The ring's
 // blocks are whole, 64-aligned blocks of the batch (the dispatch guarantees more than 32 packets
 // per wave), so classifying each block here again (oct_block) finds exactly the ring's packets.
 // (In the first launch, after long_body, this measured slower: that kernel's registers are sized
 // for its rings.)
 __global__ __launch_bounds__(256) void icrc_rx_sweep_kernel(BatchParams p) {
     __shared__ uint32_t sh_all[4 * 64 * kRxStride];
-    // nothing left by the ring's tail loop in this call (the long packets' descriptors are long_body's)
-    if (p.rx_flag && *reinterpret_cast<volatile const uint32_t *>(p.rx_flag) < p.rx_gen) return;
+    // rx_flag[0]: the ring's tail loop left short packets; rx_flag[1]: a dense long-packet range left
+    // its long packets (long_body; a sparse range's long packets have their descriptors already, and
+    // writing them again here writes the same bytes)
+    bool all_long = true;
+    if (p.rx_flag) {
+        const bool tail = *reinterpret_cast<volatile const uint32_t *>(p.rx_flag) >= p.rx_gen;
+        all_long = *reinterpret_cast<volatile const uint32_t *>(p.rx_flag + 1) >= p.rx_gen;
+        if (!tail && !all_long) return;
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *sh = sh_all + wave * 64u * kRxStride;
@@ -1098,7 +1106,7 @@ __global__ __launch_bounds__(256) void icrc_rx_sweep_kernel(BatchParams p) {
         const uint32_t L = valid ? (p.len ? p.len[i] : p.ulen) : 0u;
         OctBlock B;
         oct_block<kVerify>(p, B, off, L, valid, base, 0, lane);
-        const uint64_t need = __ballot(valid && L < p.split_len) & ~B.mine;
+        const uint64_t need = __ballot(valid && (all_long || L < p.split_len)) & ~B.mine;
         if (need != 0ull) rx_desc_block(p, sh, base, p.n - base < 64u ? p.n - base : 64u, need, lane);
     }
 }
@@ -1216,8 +1224,11 @@ int launch_hybrid_rx(const BatchParams &p, int grid, int num_cu, void *stream) {
     if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     else hipLaunchKernelGGL((icrc_hybrid_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     if (hipGetLastError() != hipSuccess) return ICRC_EDEVICE;
+    // 8 workgroups per CU (its 19 KiB of LDS each: one round of workgroups on the whole GPU), each
+    // wave walking 64-packet blocks grid-stride: most calls' sweep has nothing to do and returns at
+    // once, and half the workgroups of the round-5 grid start in half the time (4.9 us measured with 16)
     const uint64_t want = (static_cast<uint64_t>(p.n) + 255u) / 256u;
-    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u;
+    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 8u;
     hipLaunchKernelGGL(icrc_rx_sweep_kernel, dim3(static_cast<uint32_t>(want < cap ? want : cap)), dim3(256), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
