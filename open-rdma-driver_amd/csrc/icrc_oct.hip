@@ -1224,11 +1224,10 @@ int launch_hybrid_rx(const BatchParams &p, int grid, int num_cu, void *stream) {
     if (p.trailer) hipLaunchKernelGGL((icrc_hybrid_rx_kernel<true>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     else hipLaunchKernelGGL((icrc_hybrid_rx_kernel<false>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p);
     if (hipGetLastError() != hipSuccess) return ICRC_EDEVICE;
-    // 8 workgroups per CU (its 19 KiB of LDS each: one round of workgroups on the whole GPU), each
-    // wave walking 64-packet blocks grid-stride: most calls' sweep has nothing to do and returns at
-    // once, and half the workgroups of the round-5 grid start in half the time (4.9 us measured with 16)
+    // 16 workgroups per CU: a sweep with nothing to do returns at once (4.6-4.9 us); 8 per CU saved ~1
+    // us there but cost a sweep with work 13 us (786 K x 4156 B: 50 against 37 us, profiles/r06/final/)
     const uint64_t want = (static_cast<uint64_t>(p.n) + 255u) / 256u;
-    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 8u;
+    const uint64_t cap = static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u;
     hipLaunchKernelGGL(icrc_rx_sweep_kernel, dim3(static_cast<uint32_t>(want < cap ? want : cap)), dim3(256), 0, s, p);
     return hipGetLastError() == hipSuccess ? ICRC_OK : ICRC_EDEVICE;
 }
