@@ -131,7 +131,7 @@ void *icrc_engine_stream(const icrc_engine *engine);
  *        compacting long-packet walker);
  *   301 / 302  the receive parse as one fused pass on any batch (S = 2 / S = 1).
  * Other values: ICRC_EINVAL.  The diagnostics whose results are wrong by design (15, 18, 19,
- * 21-23, 27-29, 41-53, 141-153, 241-253) exist only in the A/B library libicrc_amd_ab.so (built with
+ * 21-23, 27-30, 33, 41-53, 141-153, 241-253) exist only in the A/B library libicrc_amd_ab.so (built with
  * ICRC_AB_BUILD), which no product path loads. */
 int icrc_engine_set_kernel_variant(icrc_engine *engine, int variant);
 /* The path of host messages (scalar calls, host batches of at most 1024 packets): */

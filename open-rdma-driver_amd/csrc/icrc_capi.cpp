@@ -1208,7 +1208,8 @@ int engine_teardown(icrc_engine *e) {
     const int rc = ring_free(e);
     for (Stage &s : e->st) stage_free(s);
     combiner_free(e);
-    if (e->d_table) (void)hipFree(e->d_table);
+    // a ring kernel that did not stop still reads the W = 64 table image: it is left with the ring
+    if (rc == ICRC_OK && e->d_table) (void)hipFree(e->d_table);
     if (e->d_table_oct) (void)hipFree(e->d_table_oct);
     if (e->d_rx_flag) (void)hipFree(e->d_rx_flag);
     if (e->stream) (void)hipStreamDestroy(e->stream);

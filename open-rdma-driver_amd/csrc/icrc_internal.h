@@ -91,14 +91,14 @@ constexpr int kRxVariantBase = 300;
 // Variants a batch can be forced to (icrc_engine_set_kernel_variant).  The product library
 // accepts only result-exact ones: 0, 13, 16, 17 (one packet per wave) and 40 (oct).  The A/B
 // library (built with ICRC_AB_BUILD: _build/libicrc_amd_ab.so, for measurement scripts and the
-// bench's loads-only denominator) adds the diagnostics 15, 18, 19, 21-23, 27-29, 41-53, whose results are
+// bench's loads-only denominator) adds the diagnostics 15, 18, 19, 21-23, 27-30, 33, 41-53, whose results are
 // wrong by design (49 and 51 are exact on strided batches only / on all batches, 48, 52 and 53
 // exact, but ablations all the same).
 #ifdef ICRC_AB_BUILD
 inline bool is_batch_variant(int v) {
     switch (v) {
     case 0: case 13: case 15: case 16: case 17: case 18: case 19: case 21: case 22: case 23:
-    case 27: case 28: case 29:
+    case 27: case 28: case 29: case 30: case 33:
     case 40: case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48: case 49: case 50: case 51: case 52: case 53:
         return true;
     default:

@@ -766,6 +766,15 @@ __global__ __launch_bounds__(kThreadsPerGroup) void icrc_fixed_cost_kernel(Batch
     v = __builtin_amdgcn_readfirstlane(v);
     if (lane == 0 && gw < p.n) store_result<MODE>(p, gw, v);
 }
+// (variants 30 / 33) the launch alone without the LDS image, 1024- / 256-thread workgroups (a wave
+// per packet either way: the grid scales with the block): what the 160 KiB allocation and the
+// workgroup size cost an empty launch
+template <int MODE>
+__global__ void icrc_empty_kernel(BatchParams p) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (lane == 0 && gw < p.n) store_result<MODE>(p, gw, gw);
+}
 #endif
 
 }  // namespace
@@ -809,6 +818,8 @@ static void launch_mode(const BatchParams &p, int grid, hipStream_t s) {
     case 27: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 0>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     case 28: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 1>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
     case 29: hipLaunchKernelGGL((icrc_fixed_cost_kernel<MODE, 2>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 30: hipLaunchKernelGGL((icrc_empty_kernel<MODE>), dim3(grid), dim3(kThreadsPerGroup), 0, s, p); break;
+    case 33: hipLaunchKernelGGL((icrc_empty_kernel<MODE>), dim3(grid * 4), dim3(256), 0, s, p); break;
     case 41: (void)launch_oct(MODE, p, grid, s, 1); break;  // diagnostic: loads only
     case 42: (void)launch_oct(MODE, p, grid, s, 2); break;  // diagnostic: row steps only
     case 43: (void)launch_oct(MODE, p, grid, s, 3); break;  // diagnostic: control + final products

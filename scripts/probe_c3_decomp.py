@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """configs[3] fixed cost, decomposed.  The 16 MiB WRITE (4096 packets, one per
 wave of the 256 x 1024-thread grid) through the A/B library's cut kernels, same grid / block / LDS:
-  27 the launch alone, 28 + the LDS table image, 29 + each wave's (offset, length) load,
+  30 / 33 the launch alone without LDS (1024- / 256-thread workgroups), 27 the launch alone,
+  28 + the LDS table image, 29 + each wave's (offset, length) load,
   19 the batch kernel's loads only (meta, table, row loads, ring; no CRC), 16 the product kernel.
 For compute (with and without write_trailer) and verify (zero_trailer), ragged arrays as bench.py's
 configs.c3 passes them, and the same packets as a strided batch of the MIDDLE length.  Prints one
@@ -45,7 +46,7 @@ def main():
     }
     for rnd in range(2):
         for name, fn in cases.items():
-            for v in (27, 28, 29, 19, 16, -1):
+            for v in (30, 33, 27, 28, 29, 19, 16, -1):
                 eng.set_variant(v)
                 for _ in range(20):
                     fn()

@@ -1318,7 +1318,7 @@ def test_split_batches_concurrent_streams(engine):
     assert not errors, errors
 
 
-DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 23, 27, 28, 29, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 141, 146, 148, 241)
+DIAGNOSTIC_VARIANTS = (15, 18, 19, 21, 22, 23, 27, 28, 29, 30, 33, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 141, 146, 148, 241)
 
 
 def test_kernel_variant_validation(engine, ab_engine):
