@@ -1008,6 +1008,51 @@ def test_rx_parse_mixed_mtu_stream_full(engine):
     assert len(set(want["payload_len"].tolist())) > 100  # the ragged LAST packets' lengths
 
 
+@pytest.mark.parametrize("zero_trailer", [False, True])
+def test_rx_parse_dense_and_sparse_long_ranges(engine, zero_trailer):
+    """The ragged receive's two descriptor paths for long packets in one batch: a first region of
+    4156-B packets (waves walking it take the dense C1 ring, raise the sweep's second flag and leave
+    every long packet's descriptor to the sweep), then a region of 316-B packets with one 4156-B or
+    2001-B packet per ~60 (waves there take the sparse walk and write their long packets'
+    descriptors themselves; the sweep rewrites them with the same bytes).  Every descriptor, ok
+    byte and trailer against the oracle."""
+    import icrc_amd
+
+    rng = np.random.default_rng(4242 + int(zero_trailer))
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_dense = n_cu * 16 * 64 // 4  # about a quarter of the grid's waves on all-long ranges
+    n_sparse = n_cu * 16 * 64 * 3 // 4
+    lens = np.concatenate([np.full(n_dense, 4156, np.uint32),
+                           np.where(rng.random(n_sparse) < 1 / 60, rng.choice([4156, 2001], n_sparse), 316)
+                           .astype(np.uint32)])
+    n = lens.size
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(((lens[:-1].astype(np.uint64) + 3) // 4) * 4)
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    # BTH of an RC WRITE_MIDDLE (opcode 0x07, transport RC, pad 0) on every packet: most parse OK
+    buf[off.astype(np.int64) + 28] = 0x07
+    buf[off.astype(np.int64) + 29] = 0x00
+    ic = oracle.compute_icrc_batch(buf, off, lens)
+    tr = (off + lens - 4).astype(np.int64)
+    for k in range(4):
+        buf[tr + k] = ((ic >> (8 * k)) & 0xFF).astype(np.uint8)
+    buf[tr[::53]] ^= 0x04
+    ref = buf.copy()
+    want = oracle.rx_parse(ref, off, lens, zero_trailer=zero_trailer)
+    d_buf = dev(buf)
+    d_off, d_len = dev(off), dev(lens)
+    d_desc = torch.zeros(n * 72, dtype=torch.uint8, device="cuda")
+    d_ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    engine.rx_parse(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_desc.data_ptr(), d_ok.data_ptr(),
+                    zero_trailer=zero_trailer, stream=stream_handle())
+    torch.cuda.synchronize()
+    got = d_desc.cpu().numpy().view(icrc_amd.RX_DESC_DTYPE)
+    assert_desc_equal(got, want)
+    np.testing.assert_array_equal(d_ok.cpu().numpy(), want["icrc_ok"])
+    np.testing.assert_array_equal(d_buf.cpu().numpy(), ref)
+    assert int(np.sum(want["icrc_ok"] == 0)) >= n // 53 and int(np.sum(want["status"] == 0)) > n // 2
+
+
 def test_send_receive_roundtrip(engine):
     """Packetize 24 WRITE / READ RESPONSE messages on the GPU, parse them on the GPU, and place each
     payload at its RETH va: the memory region equals the source bytes (C3 closed on-device)."""
