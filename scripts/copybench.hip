@@ -145,6 +145,117 @@ __global__ void flat_x4(const uint4 *s, uint4 *d, size_t n16) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) d[i] = s[i];
 }
 
+// COPY_ORDER=1 forms (round 6, what separates the packetizer's shape from flat_x4):
+// flat_slots<E>: the flat grid-stride order, but each E-byte element lands in the packetizer's
+// wire slots (payload element c of packet c / (kPay / E) at slot offset kHdr + ...): the flat
+// copy's order with the packetizer's layout
+template <int E, uint32_t WIRE = kWire, uint32_t HDR = kHdr>
+__global__ void flat_slots(const uint8_t *src, uint8_t *dst) {
+    constexpr uint32_t per = kPay / E;
+    const size_t n = (size_t)kN * per;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t q = i / per, k = i % per;
+        uint8_t *d = dst + q * WIRE + HDR + k * E;
+        const uint8_t *s = src + i * E;
+        if constexpr (E == 16) {
+            typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<v4 *>(d) = *reinterpret_cast<const v4 *>(s);
+        } else {
+            *reinterpret_cast<uint32_t *>(d) = *reinterpret_cast<const uint32_t *>(s);
+        }
+    }
+}
+
+// The packetizer's WHOLE write set (header 56 B + payload + 4-B trailer: contiguous 4156-B packets,
+// every byte written) without the CRC:
+// rows_full: one wave per packet (contiguous chunks, a two-packet register ring), 17 dword rows of
+// 256 B from the packet's first byte; flat_out: the flat grid-stride order over the output stream
+// (16-B aligned stores, every output line whole), each dword from the payload or a constant
+__global__ __launch_bounds__(1024) void rows_full(const uint8_t *src, uint8_t *dst, uint32_t waves) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t chunk = (kN + waves - 1) / waves;
+    const uint32_t lo = gw * chunk;
+    if (lo >= kN) return;
+    const uint32_t nq = kN - lo < chunk ? kN - lo : chunk;
+    constexpr int R = 17;
+    uint32_t ua[R], ub[R];
+    auto load = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)(lo + q) * kPay), 0, (int)kPay, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int o = (int)(4u * lane + 256u * j) - (int)kHdr;
+            u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, o >= 0 ? o : (int)0x80000000, 0, 0);
+        }
+    };
+    auto store = [&](uint32_t q, uint32_t (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)(lo + q) * kWire), 0, (int)kWire, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint32_t o = 4u * lane + 256u * j;
+            const uint32_t v = o < kHdr ? 0x11223344u : o >= kHdr + kPay ? 0xA5A5A5A5u : u[j];
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)o, 0, 0);
+        }
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        store(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        store(q + 1, ub);
+    }
+}
+
+__global__ void flat_out(const uint32_t *src, uint4 *dst) {
+    const uint32_t n16 = kN * (kWire / 4) / 4;  // 16-B output chunks (kWire is a multiple of 4, kN of 4)
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += gridDim.x * blockDim.x) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = 16u * c + 4u * k;  // < 2^32: 786432 x 4156 B
+            const uint32_t q = p / kWire, w = p - q * kWire;
+            v[k] = w < kHdr ? 0x11223344u : w >= kHdr + kPay ? 0xA5A5A5A5u : src[(q * kPay + w - kHdr) / 4u];
+        }
+        dst[c] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// quarter_rows<QR>: one wave per QR 256-B dword rows of a packet (QR = 4: a 1 KiB quarter, four
+// waves per packet), units walked in the grid's order (unit g + k * waves), each unit's loads then
+// its stores, two units in flight per wave
+template <int QR>
+__global__ __launch_bounds__(1024) void quarter_rows(const uint8_t *src, uint8_t *dst, uint32_t waves) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr uint32_t per = 16 / QR;  // units per packet
+    const uint32_t units = kN * per;
+    const uint32_t nq = gw < units ? (units - gw + waves - 1) / waves : 0u;
+    uint32_t ua[QR], ub[QR];
+    auto load = [&](uint32_t q, uint32_t (&u)[QR]) {
+        const uint32_t g = gw + q * waves;
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)(g / per) * kPay), 0, (int)kPay, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < QR; ++j) u[j] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * lane + 256u * (QR * (g % per) + j)), 0, 0);
+    };
+    auto store = [&](uint32_t q, uint32_t (&u)[QR]) {
+        const uint32_t g = gw + q * waves;
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)(g / per) * kWire), 0, (int)kWire, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < QR; ++j)
+            __builtin_amdgcn_raw_buffer_store_b32(u[j], rs, (int)(kHdr + 4u * lane + 256u * (QR * (g % per) + j)), 0, 0);
+    };
+    if (nq == 0) return;
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        store(q, ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        store(q + 1, ub);
+    }
+}
+
 template <class F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -183,6 +294,46 @@ int main() {
         printf("{\"form\": \"%s\", \"ms\": %.4f, \"GB/s (read+write)\": %.1f}\n", name, ms, wire_bytes / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
+    if (getenv("COPY_ORDER")) {  // which part of the access order separates the packetizer from flat_x4
+        const size_t n16 = (size_t)kN * kPay / 16;
+        for (int rep = 0; rep < 2; ++rep) {
+            report("flat_x4 contiguous 16 waves/CU (256-thread groups)",
+                   time_it([&] { flat_x4<<<cus * 4, 256>>>((const uint4 *)src, (uint4 *)dst, n16); }, reps));
+            report("flat_x4 contiguous 16 waves/CU (1024-thread groups)",
+                   time_it([&] { flat_x4<<<cus, 1024>>>((const uint4 *)src, (uint4 *)dst, n16); }, reps));
+            report("flat_slots x4: flat order, wire slots (256-thread groups)",
+                   time_it([&] { flat_slots<16><<<cus * 4, 256>>>(src, dst); }, reps));
+            report("flat_slots x4: flat order, slots of 4160 B, payload at 0 (line-aligned, a line skipped per slot)",
+                   time_it([&] { flat_slots<16, 4160, 0><<<cus * 4, 256>>>(src, dst); }, reps));
+            report("flat_slots x4: flat order, slots of 4096 B (contiguous, the slot index math)",
+                   time_it([&] { flat_slots<16, 4096, 0><<<cus * 4, 256>>>(src, dst); }, reps));
+            report("flat_slots x4: flat order, slots of 4160 B, payload at 56 (stores 8 B off their lines)",
+                   time_it([&] { flat_slots<16, 4160, 56><<<cus * 4, 256>>>(src, dst); }, reps));
+            report("flat_slots x4: flat order, slots of 4156 B, payload at 0 (4 B steps, no header gap)",
+                   time_it([&] { flat_slots<16, 4156, 0><<<cus * 4, 256>>>(src, dst); }, reps));
+            report("rows_dword: a wave per packet, slots of 4096 B (contiguous)",
+                   time_it([&] { rows_dword<0, false, 0, 4096, 0><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("rows_x4: a wave per packet (1 KiB rows), slots of 4156 B at 56, grid order",
+                   time_it([&] { rows_x4<0, true><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("quarter_rows 4: a wave per 1 KiB quarter, grid order",
+                   time_it([&] { quarter_rows<4><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("quarter_rows 8: a wave per 2 KiB half, grid order",
+                   time_it([&] { quarter_rows<8><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("quarter_rows 16: a wave per packet, grid order",
+                   time_it([&] { quarter_rows<16><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("rows_dword 16 waves/CU (the packetizer's copy shape)",
+                   time_it([&] { rows_dword<0><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("rows_full: a wave per packet, the whole 4156-B packet written (header, payload, trailer)",
+                   time_it([&] { rows_full<<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("flat_out: flat order over the output stream, whole packets, 16-B aligned stores",
+                   time_it([&] { flat_out<<<cus * 4, 256>>>((const uint32_t *)src, (uint4 *)dst); }, reps));
+            report("hipMemcpyDtoD contiguous",
+                   time_it([&] { CK(hipMemcpyAsync(dst, src, (size_t)kN * kPay, hipMemcpyDeviceToDevice, 0)); }, reps));
+        }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         {
             // read shape (C1): 1 Mi x 4156 B of src
