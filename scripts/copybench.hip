@@ -207,6 +207,43 @@ __global__ __launch_bounds__(1024) void rows_full(const uint8_t *src, uint8_t *d
     }
 }
 
+// rows_wg: the whole packet written, one WORKGROUP per packet (wave w takes row w of the 17, wave 0
+// also row 16), workgroups walking packets in the grid's order (g, g + G, ...): all rows of a
+// packet leave together, and the grid writes a window of G packets at a time.  The next packet's
+// row is loaded before the current one is stored.
+__global__ __launch_bounds__(1024) void rows_wg(const uint8_t *src, uint8_t *dst) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t o0 = 4u * lane + 256u * w, o1 = 4u * lane + 256u * 16u;  // row w; row 16 (wave 0)
+    auto ld = [&](uint32_t q, uint32_t o) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)q * kPay), 0, (int)kPay, 0x00020000);
+        const int s = (int)o - (int)kHdr;
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, s >= 0 ? s : (int)0x80000000, 0, 0);
+    };
+    auto st = [&](uint32_t q, uint32_t o, uint32_t u) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)q * kWire), 0, (int)kWire, 0x00020000);
+        const uint32_t v = o < kHdr ? 0x11223344u : o >= kHdr + kPay ? 0xA5A5A5A5u : u;
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)o, 0, 0);
+    };
+    uint32_t q = blockIdx.x;
+    if (q >= kN) return;
+    uint32_t a0 = ld(q, o0), a1 = w == 0 ? ld(q, o1) : 0u;
+    for (;;) {
+        const uint32_t qn = q + gridDim.x;
+        uint32_t b0 = 0, b1 = 0;
+        if (qn < kN) {
+            b0 = ld(qn, o0);
+            if (w == 0) b1 = ld(qn, o1);
+        }
+        st(q, o0, a0);
+        if (w == 0) st(q, o1, a1);
+        if (qn >= kN) break;
+        q = qn;
+        a0 = b0;
+        a1 = b1;
+    }
+}
+
 __global__ void flat_out(const uint32_t *src, uint4 *dst) {
     const uint32_t n16 = kN * (kWire / 4) / 4;  // 16-B output chunks (kWire is a multiple of 4, kN of 4)
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += gridDim.x * blockDim.x) {
@@ -327,6 +364,10 @@ int main() {
                    time_it([&] { rows_full<<<cus, 1024>>>(src, dst, cus * 16); }, reps));
             report("flat_out: flat order over the output stream, whole packets, 16-B aligned stores",
                    time_it([&] { flat_out<<<cus * 4, 256>>>((const uint32_t *)src, (uint4 *)dst); }, reps));
+            report("rows_wg: a workgroup per packet (a wave per row), whole packets, grid order",
+                   time_it([&] { rows_wg<<<cus, 1024>>>(src, dst); }, reps));
+            report("rows_wg: a workgroup per packet, 2 workgroups per CU",
+                   time_it([&] { rows_wg<<<cus * 2, 1024>>>(src, dst); }, reps));
             report("hipMemcpyDtoD contiguous",
                    time_it([&] { CK(hipMemcpyAsync(dst, src, (size_t)kN * kPay, hipMemcpyDeviceToDevice, 0)); }, reps));
         }
