@@ -171,17 +171,20 @@ __global__ void flat_slots(const uint8_t *src, uint8_t *dst) {
 // rows_full: one wave per packet (contiguous chunks, a two-packet register ring), 17 dword rows of
 // 256 B from the packet's first byte; flat_out: the flat grid-stride order over the output stream
 // (16-B aligned stores, every output line whole), each dword from the payload or a constant
+// (IL: packet q of the wave is gw + q * waves, the grid's order; SAUX: the stores' cache policy)
+template <bool IL = false, int SAUX = 0>
 __global__ __launch_bounds__(1024) void rows_full(const uint8_t *src, uint8_t *dst, uint32_t waves) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t chunk = (kN + waves - 1) / waves;
-    const uint32_t lo = gw * chunk;
-    if (lo >= kN) return;
-    const uint32_t nq = kN - lo < chunk ? kN - lo : chunk;
+    if (gw * chunk >= kN) return;
+    const uint32_t lo = IL ? gw : gw * chunk;
+    const uint32_t nq = IL ? (kN - gw + waves - 1) / waves : (kN - lo < chunk ? kN - lo : chunk);
+    auto pkt = [&](uint32_t q) -> size_t { return IL ? (size_t)gw + (size_t)q * waves : (size_t)(lo + q); };
     constexpr int R = 17;
     uint32_t ua[R], ub[R];
     auto load = [&](uint32_t q, uint32_t (&u)[R]) {
-        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + (size_t)(lo + q) * kPay), 0, (int)kPay, 0x00020000);
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + pkt(q) * kPay), 0, (int)kPay, 0x00020000);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const int o = (int)(4u * lane + 256u * j) - (int)kHdr;
@@ -189,12 +192,12 @@ __global__ __launch_bounds__(1024) void rows_full(const uint8_t *src, uint8_t *d
         }
     };
     auto store = [&](uint32_t q, uint32_t (&u)[R]) {
-        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + (size_t)(lo + q) * kWire), 0, (int)kWire, 0x00020000);
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(dst + pkt(q) * kWire), 0, (int)kWire, 0x00020000);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const uint32_t o = 4u * lane + 256u * j;
             const uint32_t v = o < kHdr ? 0x11223344u : o >= kHdr + kPay ? 0xA5A5A5A5u : u[j];
-            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)o, 0, SAUX);
         }
     };
     load(0, ua);
@@ -362,6 +365,14 @@ int main() {
                    time_it([&] { rows_dword<0><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
             report("rows_full: a wave per packet, the whole 4156-B packet written (header, payload, trailer)",
                    time_it([&] { rows_full<<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("rows_full, packets in the grid's order",
+                   time_it([&] { rows_full<true><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
+            report("rows_full, 32 waves per CU",
+                   time_it([&] { rows_full<<<cus * 2, 1024>>>(src, dst, cus * 32); }, reps));
+            report("rows_full, packets in the grid's order, 32 waves per CU",
+                   time_it([&] { rows_full<true><<<cus * 2, 1024>>>(src, dst, cus * 32); }, reps));
+            report("rows_full, nt stores",
+                   time_it([&] { rows_full<false, 2><<<cus, 1024>>>(src, dst, cus * 16); }, reps));
             report("flat_out: flat order over the output stream, whole packets, 16-B aligned stores",
                    time_it([&] { flat_out<<<cus * 4, 256>>>((const uint32_t *)src, (uint4 *)dst); }, reps));
             report("rows_wg: a workgroup per packet (a wave per row), whole packets, grid order",
