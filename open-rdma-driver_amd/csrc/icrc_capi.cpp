@@ -193,6 +193,7 @@ struct DispatchKnobs {
     int long_self = 1;           // ICRC_AB_LONG_SELF=0: the two workgroup sets (oct, then long-packet ones)
     int self_grid_mult = 1;      // ICRC_AB_SELF_GRID: workgroups per CU of the in-place hybrid (smaller ranges)
     int long_walk = 0;           // ICRC_AB_LONG_WALK=1: run_walk_masked (icrc_long.h; measured, rejected)
+    int small_ppw = 2;           // packets per wave of a small batch's grid (ICRC_AB_SMALL_PPW)
 };
 DispatchKnobs dispatch_knobs() {
     DispatchKnobs k;
@@ -212,6 +213,7 @@ DispatchKnobs dispatch_knobs() {
     k.long_self = env("ICRC_AB_LONG_SELF", 1);
     k.self_grid_mult = std::max(1, std::min(8, env("ICRC_AB_SELF_GRID", 1)));
     k.long_walk = env("ICRC_AB_LONG_WALK", 0);
+    k.small_ppw = std::max(1, std::min(16, env("ICRC_AB_SMALL_PPW", 2)));
 #endif
     return k;
 }
@@ -244,9 +246,15 @@ int dispatch(icrc_engine *e, int mode, BatchParams p, void *stream) {
     // Small batches (at most one packet per wave of the grid, e.g. a 16 MiB message = 4096 packets):
     // the one-packet pipeline alone — packing short packets eight to a wave buys nothing when
     // every packet has a wave of its own, and the split's second launch and fork / join cost more
-    // than the kernels (C3 round trip 0.069 -> 0.020 ms).
+    // than the kernels (C3 round trip 0.069 -> 0.020 ms).  Two packets per wave (one set of the
+    // pipeline: both packets' rows in flight together) on half the workgroups: C3 9.9 -> 9.6 us per
+    // launch (rocprof), 4 or 8 per wave 13.5 / 21 us (profiles/r06/c3/c3_grid_ppw.jsonl).
     if (!hybrid_forced && p.n <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup) {
         p.variant = icrc::kDefaultVariant;
+        if (k.small_ppw > 1 && !p.spread) {
+            const uint32_t per_wg = icrc::kWavesPerGroup * static_cast<uint32_t>(k.small_ppw);
+            return icrc::launch_batch(mode, p, static_cast<int>(std::max<uint32_t>(1u, (p.n + per_wg - 1) / per_wg)), stream);
+        }
         return icrc::launch_batch(mode, p, grid, stream);
     }
     p.long_variant = e->variant >= icrc::kHybridCompactBase && hybrid_forced ? 1 : 0;
