@@ -131,6 +131,58 @@ __global__ __launch_bounds__(1024) void read_rows(const uint8_t *src, uint32_t *
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// COPY_READ=1 forms (round 6): the C1 read set (1 Mi x 4156-B packets, 4152 B read each) with
+// wider lanes: E = 8 / 16 bytes per lane (512-B / 1-KiB rows, 9 / 5 row loads per packet, the last
+// partial), one wave per packet, two packets in flight; and a flat grid-stride 16-B read of the same
+// bytes (XOR fold, stored only on a magic value)
+template <int E>
+__global__ __launch_bounds__(1024) void read_rows_w(const uint8_t *src, uint32_t *out, uint32_t waves, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t chunk = (n + waves - 1) / waves;
+    if (gw * chunk >= n) return;
+    const uint32_t nq = n - gw * chunk < chunk ? n - gw * chunk : chunk;
+    constexpr int R = (4152 + 64 * E - 1) / (64 * E);
+    typedef uint32_t vv __attribute__((ext_vector_type(E / 4)));
+    vv ua[R], ub[R];
+    uint32_t acc = 0;
+    auto load = [&](uint32_t q, vv (&u)[R]) {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + ((size_t)gw * chunk + q) * 4156u), 0, 4152, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int o = (int)(E * lane + 64 * E * j);
+            if constexpr (E == 16) u[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 2);
+            else u[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 2);
+        }
+    };
+    auto fold = [&](vv (&u)[R]) {
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+            for (int k = 0; k < E / 4; ++k) acc ^= u[j][k];
+    };
+    load(0, ua);
+    for (uint32_t q = 0; q < nq; q += 2) {
+        if (q + 1 < nq) load(q + 1, ub);
+        fold(ua);
+        if (q + 1 >= nq) break;
+        if (q + 2 < nq) load(q + 2, ua);
+        fold(ub);
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void flat_read_x4(const uint4 *s, size_t n16, uint32_t *out) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const v4 *p = reinterpret_cast<const v4 *>(s);
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const v4 v = __builtin_nontemporal_load(p + i);
+        acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // COPY_RAND=1: the source filled with splitmix64 bytes instead of a constant
 __global__ void fill_rand(uint64_t *p, size_t n8) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
@@ -334,6 +386,27 @@ int main() {
         printf("{\"form\": \"%s\", \"ms\": %.4f, \"GB/s (read+write)\": %.1f}\n", name, ms, wire_bytes / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
+    if (getenv("COPY_READ")) {  // the C1 read set with wider lanes, and a flat read of the same bytes
+        const uint32_t n = 1048576u;
+        const double rb = (double)n * 4152;
+        uint32_t *o = (uint32_t *)dst;
+        auto rep_r = [&](const char *name, float ms) {
+            printf("{\"form\": \"%s\", \"ms\": %.4f, \"GB/s (read)\": %.1f}\n", name, ms, rb / (ms * 1e-3) / 1e9);
+            fflush(stdout);
+        };
+        for (int rep = 0; rep < 3; ++rep) {
+            rep_r("read C1 shape: dword rows (256 B), a wave per packet", time_it([&] { read_rows<false><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
+            rep_r("read C1 set: dwordx2 rows (512 B), a wave per packet", time_it([&] { read_rows_w<8><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
+            rep_r("read C1 set: dwordx4 rows (1 KiB), a wave per packet", time_it([&] { read_rows_w<16><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
+            rep_r("flat grid-stride 16-B nt reads of the same byte count (256-thread groups, 16 waves/CU)",
+                  time_it([&] { flat_read_x4<<<cus * 4, 256>>>((const uint4 *)src, (size_t)rb / 16, o); }, reps));
+            rep_r("flat grid-stride 16-B nt reads of the same byte count (32 waves/CU)",
+                  time_it([&] { flat_read_x4<<<cus * 8, 256>>>((const uint4 *)src, (size_t)rb / 16, o); }, reps));
+        }
+        CK(hipFree(src));
+        CK(hipFree(dst));
+        return 0;
+    }
     if (getenv("COPY_ORDER")) {  // which part of the access order separates the packetizer from flat_x4
         const size_t n16 = (size_t)kN * kPay / 16;
         for (int rep = 0; rep < 2; ++rep) {
