@@ -135,14 +135,16 @@ __global__ __launch_bounds__(1024) void read_rows(const uint8_t *src, uint32_t *
 // wider lanes: E = 8 / 16 bytes per lane (512-B / 1-KiB rows, 9 / 5 row loads per packet, the last
 // partial), one wave per packet, two packets in flight; and a flat grid-stride 16-B read of the same
 // bytes (XOR fold, stored only on a magic value)
-template <int E>
+// SHIFT: the loads start SHIFT bytes before the packet (end-aligned rows of a kernel: 968 B for x4
+// rows of 4156-B packets, 456 for x2); lanes wholly before the packet read out of range (0)
+template <int E, int SHIFT = 0>
 __global__ __launch_bounds__(1024) void read_rows_w(const uint8_t *src, uint32_t *out, uint32_t waves, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t chunk = (n + waves - 1) / waves;
     if (gw * chunk >= n) return;
     const uint32_t nq = n - gw * chunk < chunk ? n - gw * chunk : chunk;
-    constexpr int R = (4152 + 64 * E - 1) / (64 * E);
+    constexpr int R = (4152 + SHIFT + 64 * E - 1) / (64 * E);
     typedef uint32_t vv __attribute__((ext_vector_type(E / 4)));
     vv ua[R], ub[R];
     uint32_t acc = 0;
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(1024) void read_rows_w(const uint8_t *src, uint32_t
         auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(src + ((size_t)gw * chunk + q) * 4156u), 0, 4152, 0x00020000);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const int o = (int)(E * lane + 64 * E * j);
+            const int o0 = (int)(E * lane + 64 * E * j) - SHIFT;
+            const int o = o0 >= 0 ? o0 : (int)0x80000000;
             if constexpr (E == 16) u[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 2);
             else u[j] = __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 2);
         }
@@ -398,6 +401,8 @@ int main() {
             rep_r("read C1 shape: dword rows (256 B), a wave per packet", time_it([&] { read_rows<false><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
             rep_r("read C1 set: dwordx2 rows (512 B), a wave per packet", time_it([&] { read_rows_w<8><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
             rep_r("read C1 set: dwordx4 rows (1 KiB), a wave per packet", time_it([&] { read_rows_w<16><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
+            rep_r("read C1 set: dwordx4 rows end-aligned (968 B shift, 8 B off 16)", time_it([&] { read_rows_w<16, 968><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
+            rep_r("read C1 set: dwordx2 rows end-aligned (456 B shift)", time_it([&] { read_rows_w<8, 456><<<cus, 1024>>>(src, o, cus * 16, n); }, reps));
             rep_r("flat grid-stride 16-B nt reads of the same byte count (256-thread groups, 16 waves/CU)",
                   time_it([&] { flat_read_x4<<<cus * 4, 256>>>((const uint4 *)src, (size_t)rb / 16, o); }, reps));
             rep_r("flat grid-stride 16-B nt reads of the same byte count (32 waves/CU)",
