@@ -1283,6 +1283,40 @@ def test_tiny_batches_every_path(engine, n, variant):
     np.testing.assert_array_equal(out, oracle_icrcs(buf, off, lens))
 
 
+@pytest.mark.parametrize("delta", [-4095, -4063, -1, 0, 1])
+def test_small_batch_grid_boundary(engine, delta):
+    """The small-batch dispatch (at most one packet per wave of the full grid: two packets per wave
+    on half the workgroups, round 6) at and around its bound of #CUs x 16 packets (n = #CUs x 16 +
+    delta, at least 1: 1, 33, bound - 1, the bound, bound + 1 on 256 CUs): mixed lengths with short
+    (error) and long packets, 3 % misaligned offsets; compute with write_trailer, then verify with
+    zero_trailer, against the oracle (ICRCs, written trailers, verify results, zeroed trailers)."""
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    n = max(1, n_cu * 16 + delta)
+    rng = np.random.default_rng(7100 + n)
+    lens = rng.choice([40, 44, 61, 316, 1084, 1089, 4156, 9000], n, p=[.02, .05, .1, .3, .2, .03, .25, .05]).astype(np.uint32)
+    gap = np.where(rng.random(n) < 0.03, rng.integers(1, 4, n), 0).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(((lens[:-1].astype(np.uint64) + 3) // 4) * 4 + gap[:-1])
+    buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 8, dtype=np.uint8)
+    ok_len = lens >= 44
+    out, nerr, wrote = run_batch(engine, buf, off, lens, write_trailer=True)
+    want = oracle_icrcs(buf, off[ok_len], lens[ok_len])
+    np.testing.assert_array_equal(out[ok_len], want)
+    assert nerr == int((~ok_len).sum())
+    tr = (off[ok_len] + lens[ok_len] - 4).astype(np.int64)
+    got_tr = wrote[tr] | (wrote[tr + 1].astype(np.uint32) << 8) | (wrote[tr + 2].astype(np.uint32) << 16) | \
+        (wrote[tr + 3].astype(np.uint32) << 24)
+    np.testing.assert_array_equal(got_tr, want)
+    d_buf, d_off, d_len = dev(wrote), dev(off), dev(lens)
+    d_ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    engine.verify_batch(d_buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_ok.data_ptr(), True, 0, stream_handle())
+    torch.cuda.synchronize()
+    ok = d_ok.cpu().numpy()
+    assert np.all(ok[ok_len] == 1) and np.all(ok[~ok_len] == 0xFF)
+    after = d_buf.cpu().numpy()
+    assert not any(after[tr + k].any() for k in range(4))
+
+
 def test_oct_frame_boundaries(engine):
     """The oct kernel's frame arithmetic at its edges, through the default hybrid dispatch (a batch
     big enough to split): 1- and 2-frame packets (L = 320 / 324: 10 / 11 rows), 4 frames (1084,
