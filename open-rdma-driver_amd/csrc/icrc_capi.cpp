@@ -1551,7 +1551,15 @@ int icrc_rx_parse_device(icrc_engine *e, uint8_t *d_base, const uint64_t *d_off,
     // two passes (786 K x 4156 B: 0.70 vs 0.59 ms, profiles/r02_rx_fused_ab.jsonl).
     if (e->variant < 0 && n <= static_cast<uint32_t>(e->num_cu) * icrc::kWavesPerGroup) {
         p.variant = 2;
-        return icrc::launch_rx(p, grid_for(e, n), stream);
+        // (A/B, ICRC_AB_RX_SMALL_PPW: packets per wave of this grid, as the compute dispatch's small
+        // batches; 2 measured 1 % slower here, 4 +46 %: profiles/r06/rx/rx_small_grid_ppw.jsonl)
+        int ppw = 1;
+#ifdef ICRC_AB_BUILD
+        if (const char *v = std::getenv("ICRC_AB_RX_SMALL_PPW")) ppw = std::max(1, std::min(16, std::atoi(v)));
+#endif
+        const uint32_t per_wg = icrc::kWavesPerGroup * static_cast<uint32_t>(ppw);
+        const int grid = ppw > 1 ? static_cast<int>(std::max<uint32_t>(1u, (n + per_wg - 1) / per_wg)) : grid_for(e, n);
+        return icrc::launch_rx(p, grid, stream);
     }
     // Strided batches of short packets: ONE pass (icrc_oct_rx_kernel): the oct verify keeps each
     // packet's header words as loaded and stores the descriptors itself, so the header lines are not
